@@ -1,0 +1,94 @@
+/*
+ * uflow_frame_crc.h -- C ABI of libuflowcrc.so, the MI355X-native drop-in for uflow's
+ * per-frame CRC-32 (polynomial 0x132c00699, reflected 0x9960034C) in src/frame.
+ *
+ * Reference (lowquark/uflow v0.7.1, Rust) interfaces each entry point replaces:
+ *   ufc_crc32_compute      <- src/frame/serial/crc.rs:102-104  `pub fn compute(data: &[u8]) -> u32`
+ *   ufc_crc32_extend       <- src/frame/serial/crc.rs:94-100   `pub fn extend(initial_crc: u32, data: &[u8]) -> u32`
+ *   ufc_frame_validate     <- src/frame/serial/mod.rs:675-690  the CRC gate of `Frame::read`
+ *   ufc_frame_seal         <- src/frame/serial/mod.rs:463-470 (every fixed-size write_*) and
+ *                             src/frame/serial/build.rs:151-159 (DataFrameBuilder/AckFrameBuilder::build)
+ *   ufc_crc_batch_fixed /  <- many calls of the gate above, one per received datagram
+ *   ufc_crc_batch_varlen      (src/server/mod.rs:597-601, src/client/mod.rs:618-622), batched on the GPU
+ *   ufc_seal_batch_fixed / <- many calls of the seal above, one per emitted frame
+ *   ufc_seal_batch_varlen     (src/half_connection/emit.rs:114-125, 205-211), batched on the GPU
+ *   ufc_validate_host_varlen  the same gate for frames that start and end in host memory
+ *                             (a UDP receive buffer): H2D copy + GPU CRC + D2H copy
+ *
+ * Conventions (mirroring the reference):
+ *   - All buffers are caller-owned; nothing is retained after a call returns (device calls:
+ *     after the work queued on `stream` completes).
+ *   - A CRC mismatch is data (valid = 0), never an error -- exactly like `Frame::read`
+ *     returning None.  Errors are negative return codes for invalid arguments or HIP failures.
+ *   - Batch semantics per frame i of length len_i:
+ *         crc_out[i]   = compute(frame_i[0 .. len_i-4])      (compute(frame_i) when len_i < 4)
+ *         valid_out[i] = len_i >= 5 && crc_out[i] == BE32(frame_i[len_i-4 .. len_i])
+ *     and the seal writes BE32(compute(frame_i[0 .. len_i-4])) into frame_i[len_i-4 .. len_i].
+ *   - Device entry points are asynchronous on `stream` (a hipStream_t, or NULL for the null
+ *     stream), allocate nothing per call, and never fall back to the CPU: without a usable
+ *     MI355X (gfx950) device ufc_ctx_create fails with UFC_ERR_NO_DEVICE.
+ *   - One ufc_ctx per device per host thread; the scalar host functions are reentrant.
+ */
+#ifndef UFLOW_FRAME_CRC_H
+#define UFLOW_FRAME_CRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define UFC_OK 0
+#define UFC_ERR_INVALID_ARG (-1)
+#define UFC_ERR_NO_DEVICE (-2)
+#define UFC_ERR_HIP (-3)
+#define UFC_ERR_NOMEM (-4)
+
+/* Frame constants from the reference (src/frame/serial/mod.rs:11-13, src/lib.rs:286-294). */
+#define UFC_FRAME_CRC_SIZE 4
+#define UFC_FRAME_OVERHEAD 5
+#define UFC_MAX_FRAME_SIZE 1472
+
+/* ---- scalar host entry points (bit-exact with crc.rs; drop-in for the Rust functions) ---- */
+uint32_t ufc_crc32_compute(const uint8_t* data, size_t len);
+uint32_t ufc_crc32_extend(uint32_t initial_crc, const uint8_t* data, size_t len);
+/* 1 if the frame passes Frame::read's length + CRC gate, 0 if Frame::read would return None there. */
+int ufc_frame_validate(const uint8_t* frame, size_t len);
+/* Writes BE32(compute(frame[..len-4])) into frame[len-4..len]; UFC_ERR_INVALID_ARG if len < 4. */
+int ufc_frame_seal(uint8_t* frame, size_t len);
+
+/* ---- device context ---- */
+typedef struct ufc_ctx ufc_ctx;
+int ufc_device_count(void);
+int ufc_ctx_create(ufc_ctx** out, int device);
+int ufc_ctx_destroy(ufc_ctx* ctx);
+const char* ufc_error_string(int code);
+/* Last HIP error code seen by this context (0 if none). */
+int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
+
+/* ---- batched, device-resident ---- */
+/* Frame i occupies d_frames[i*stride .. i*stride + frame_len); stride >= frame_len.
+ * d_crc_out (n words) and d_valid_out (n bytes) are each nullable, not both. */
+int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
+                        uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream);
+/* Frame i occupies d_bytes[d_offsets[i] .. d_offsets[i+1]) (CSR, n+1 offsets, nondecreasing). */
+int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
+                         uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream);
+/* In-place seal of every frame (frame_len >= 4); d_crc_out nullable. */
+int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
+                         uint32_t* d_crc_out, void* stream);
+int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
+                          uint32_t* d_crc_out, void* stream);
+
+/* ---- host buffers in, host buffers out (the receive path of SURVEY.md config 5) ----
+ * Copies the frames through pinned staging buffers owned by the context, runs the batched
+ * gate on the device and copies crc/valid back; synchronous.  h_offsets as above. */
+int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
+                             uint32_t* h_crc_out, uint8_t* h_valid_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* UFLOW_FRAME_CRC_H */

@@ -1,0 +1,157 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) vs the CPU oracle, bit-exact.
+
+Cases follow the reference's own tests: KAT (crc.rs:135-138), lengths around every internal
+boundary of the kernel (256-byte blocks, the G/data boundary, chunking), fixed-value frames of
+every kind (serial/mod.rs:760-925), bit flips (serial/mod.rs:1054-1080), truncation and
+extra bytes (serial/mod.rs:738-758), empty/short frames (mod.rs:676-678), varlen batches.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _rand_bytes(rng, n):
+    return rng.integers(0, 256, size=n, dtype=np.uint8)
+
+
+def _fixed_case(engine, rng, frame_len, stride, n, seal_first=True, flip_every=0):
+    buf = _rand_bytes(rng, max(n * stride, 1) + 64)
+    if seal_first and frame_len >= 4:
+        oracle.seal_fixed(buf, stride, frame_len, n)
+    if flip_every:
+        for i in range(0, n, flip_every):
+            byte = i * stride + rng.integers(0, max(frame_len, 1))
+            buf[byte] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    ref_crc, ref_valid = oracle.validate_fixed(buf, stride, frame_len, n)
+    d = torch.from_numpy(buf).to(DEV)
+    crc, valid = engine.crc_fixed(d, frame_len, stride=stride, n=n)
+    torch.cuda.synchronize()
+    got_crc = crc.cpu().numpy().view(np.uint32)
+    got_valid = valid.cpu().numpy()
+    bad = np.nonzero(got_crc != ref_crc)[0]
+    assert bad.size == 0, f"len={frame_len} stride={stride} n={n}: {bad.size} crc mismatches, first {bad[:5]}"
+    assert np.array_equal(got_valid, ref_valid), f"len={frame_len} stride={stride} n={n}: valid mismatch"
+    return got_valid
+
+
+LENGTHS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 12, 13, 15, 16, 17, 31, 63, 64, 65, 100, 247, 248, 249, 250, 251, 252,
+           253, 254, 255, 256, 257, 258, 259, 260, 261, 263, 264, 500, 511, 512, 513, 515, 516, 1000, 1472, 1496,
+           1500, 1531, 1532, 1533, 1535, 1536, 1537, 1540, 1787, 1788, 2048, 3000, 8192]
+
+
+@pytest.mark.parametrize("frame_len", LENGTHS)
+def test_fixed_lengths(engine, frame_len):
+    rng = np.random.default_rng(1000 + frame_len)
+    for stride_extra in (0, 3):
+        for n in (1, 5, 67):
+            _fixed_case(engine, rng, frame_len, frame_len + stride_extra, n)
+
+
+def test_fixed_large_batch_with_flips(engine):
+    rng = np.random.default_rng(7)
+    valid = _fixed_case(engine, rng, 1500, 1500, 20000, flip_every=1000)
+    assert valid.sum() == 20000 - 20
+
+
+def test_fixed_kat(engine):
+    frame = bytearray(b"123456789" + b"\0\0\0\0")
+    oracle.frame_seal(frame)
+    assert frame[-4:] == bytes.fromhex("11A6F2A3")
+    d = torch.tensor(list(frame), dtype=torch.uint8, device=DEV)
+    crc, valid = engine.crc_fixed(d, len(frame))
+    assert int(crc.cpu().numpy().view(np.uint32)[0]) == 0x11A6F2A3
+    assert int(valid.cpu()[0]) == 1
+
+
+def test_seal_fixed(engine):
+    rng = np.random.default_rng(11)
+    for frame_len in (4, 5, 9, 14, 25, 259, 260, 1472, 1500, 2051):
+        for stride in (frame_len, frame_len + 5):
+            n = 130
+            buf = _rand_bytes(rng, n * stride + 16)
+            ref = buf.copy()
+            oracle.seal_fixed(ref, stride, frame_len, n)
+            d = torch.from_numpy(buf).to(DEV)
+            crc_out = torch.empty(n, dtype=torch.int32, device=DEV)
+            engine.seal_fixed(d, frame_len, stride=stride, n=n, crc_out=crc_out)
+            torch.cuda.synchronize()
+            assert np.array_equal(d.cpu().numpy(), ref), f"seal len={frame_len} stride={stride}"
+            ref_crc, ref_valid = oracle.validate_fixed(ref, stride, frame_len, n)
+            assert np.array_equal(crc_out.cpu().numpy().view(np.uint32), ref_crc)
+            assert ref_valid.all() or frame_len < 5
+
+
+def _varlen_case(engine, rng, lens, seal=True, flip_every=0):
+    offsets = np.zeros(len(lens) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    data = _rand_bytes(rng, int(offsets[-1]) + 1)
+    if seal:
+        oracle.seal_varlen(data, offsets.astype(np.uint64)) if all(l >= 4 for l in lens) else None
+    if flip_every:
+        for i in range(0, len(lens), flip_every):
+            if lens[i]:
+                data[offsets[i] + rng.integers(0, lens[i])] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    ref_crc, ref_valid = oracle.validate_varlen(data, offsets.astype(np.uint64))
+    crc, valid = engine.crc_varlen(torch.from_numpy(data).to(DEV), torch.from_numpy(offsets).to(DEV))
+    torch.cuda.synchronize()
+    got = crc.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(got != ref_crc)[0]
+    assert bad.size == 0, f"{bad.size} varlen crc mismatches, first idx {bad[:5]} lens {[lens[i] for i in bad[:5]]}"
+    assert np.array_equal(valid.cpu().numpy(), ref_valid)
+    return valid.cpu().numpy()
+
+
+def test_varlen_mixed(engine):
+    rng = np.random.default_rng(21)
+    lens = rng.integers(64, 1501, size=10000).tolist()
+    _varlen_case(engine, rng, lens, flip_every=97)
+
+
+def test_varlen_edges(engine):
+    rng = np.random.default_rng(22)
+    lens = [0, 1, 2, 3, 4, 5, 6, 255, 256, 257, 258, 259, 260, 1472, 8192, 0, 9, 3000, 1, 1532, 1533] * 7
+    rng.shuffle(lens)
+    _varlen_case(engine, rng, lens, seal=False)
+
+
+def test_varlen_uflow_frames(engine):
+    """Real uflow frame sizes 5..1472 B (src/lib.rs:294)."""
+    rng = np.random.default_rng(23)
+    lens = rng.integers(5, 1473, size=5000).tolist()
+    valid = _varlen_case(engine, rng, lens)
+    assert valid.all()
+
+
+def test_seal_varlen(engine):
+    rng = np.random.default_rng(31)
+    lens = rng.integers(4, 2000, size=3000).tolist()
+    offsets = np.zeros(len(lens) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    data = _rand_bytes(rng, int(offsets[-1]))
+    ref = data.copy()
+    oracle.seal_varlen(ref, offsets.astype(np.uint64))
+    d = torch.from_numpy(data).to(DEV)
+    engine.seal_varlen(d, torch.from_numpy(offsets).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), ref)
+
+
+def test_host_varlen(engine):
+    rng = np.random.default_rng(41)
+    lens = rng.integers(5, 1473, size=4000).tolist()
+    offsets = np.zeros(len(lens) + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum(lens)
+    data = _rand_bytes(rng, int(offsets[-1]))
+    oracle.seal_varlen(data, offsets)
+    data[int(offsets[10]) + 3] ^= 0x10
+    ref_crc, ref_valid = oracle.validate_varlen(data, offsets)
+    crc, valid = engine.validate_host_varlen(data, offsets)
+    assert np.array_equal(crc, ref_crc)
+    assert np.array_equal(valid, ref_valid)
+    assert valid.sum() == len(lens) - 1

@@ -1,0 +1,363 @@
+// Exploration round 2 (not product code): coalesced word-interleaved CRC chains.
+// A frame's CRC bytes are right-aligned into a virtual stream whose length is a multiple
+// of 256 B (zero pad, then G = A^-4(~0) so that the init ~0 is folded in).  Slot s (0..63)
+// owns virtual words s, s+64, s+128, ...; each slot runs a Horner chain with the constant
+// A^256 (advance 256 zero bytes) -> one replicated byte-table set in LDS; at the end slot s
+// is multiplied by A^(4(64-s)) through per-slot nibble tables, and the slots are XORed.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstdint>
+#include <vector>
+#include <algorithm>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+static const uint32_t POLY_R = 0x9960034Cu;
+static uint32_t T_ref[256], L0[256];
+static uint32_t adv(uint32_t v, int nbytes) { for (int i = 0; i < nbytes; i++) v = (v >> 8) ^ L0[v & 0xff]; return v; }
+static void build_tables() {
+  for (int i = 0; i < 256; i++) {
+    uint32_t r = ~0u ^ (uint32_t)i;
+    for (int b = 0; b < 8; b++) r = (r & 1) ? (r >> 1) ^ POLY_R : (r >> 1);
+    T_ref[i] = ~r;
+    uint32_t v = (uint32_t)i;
+    for (int b = 0; b < 8; b++) v = (v & 1) ? (v >> 1) ^ POLY_R : (v >> 1);
+    L0[i] = v;
+  }
+}
+static uint32_t crc_cpu(const uint8_t* d, size_t n) {
+  uint32_t c = 0;
+  for (size_t i = 0; i < n; i++) c = (c >> 8) ^ T_ref[(uint8_t)(c ^ d[i])];
+  return c;
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__global__ void fill_kernel(uint64_t* p, size_t nwords, uint64_t seed) {
+  size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  size_t st = (size_t)gridDim.x * blockDim.x;
+  for (; i < nwords; i += st) p[i] = splitmix64(seed ^ (i * 0x2545F4914F6CDD1Dull));
+}
+
+template <typename VT>
+__global__ __launch_bounds__(256) void m_coalesced(const VT* __restrict__ p, size_t n, uint32_t* out) {
+  size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  size_t T = (size_t)gridDim.x * blockDim.x;
+  uint32_t acc = 0;
+  #pragma unroll 8
+  for (size_t i = t; i < n; i += T) {
+    VT v = p[i];
+    const uint32_t* w = (const uint32_t*)&v;
+    #pragma unroll
+    for (int k = 0; k < (int)(sizeof(VT) / 4); k++) acc ^= w[k];
+  }
+  out[t] = acc;
+}
+
+__device__ __forceinline__ uint32_t lds_ld(const char* lds, uint32_t byteoff) {
+  return *(const uint32_t*)(lds + byteoff);
+}
+// chain step: A^256 applied to V via 4 replicated byte tables (byte k*32768 + e*128 + c*4)
+__device__ __forceinline__ uint32_t chain(const char* lds, uint32_t v, uint32_t c4) {
+  uint32_t a0 = ((v << 7) & 0x7F80u) | c4;
+  uint32_t a1 = ((v >> 1) & 0x7F80u) | c4;
+  uint32_t a2 = ((v >> 9) & 0x7F80u) | c4;
+  uint32_t a3 = ((v >> 17) & 0x7F80u) | c4;
+  return lds_ld(lds, a0) ^ lds_ld(lds, a1 + 32768) ^ lds_ld(lds, a2 + 65536) ^ lds_ld(lds, a3 + 98304);
+}
+// per-slot multiply via nibble tables: entry e of nibble k at nb + k*CS*16*4 ... (CS columns)
+template <int CS>
+__device__ __forceinline__ uint32_t nibmul(const char* lds, uint32_t v, uint32_t base) {
+  // address = base + (k*16 + e) * (CS*4)
+  constexpr int RS = CS * 4;            // row stride bytes (256 or 128)
+  constexpr int SH = (CS == 64) ? 8 : 7; // log2(RS)
+  uint32_t r = 0;
+  #pragma unroll
+  for (int k = 0; k < 8; k++) {
+    int sh = 4 * k - SH;
+    uint32_t e = (sh >= 0) ? (v >> sh) : (v << (-sh));
+    r ^= lds_ld(lds, (e & (0xFu << SH)) + base + k * 16 * RS);
+  }
+  return r;
+}
+
+
+// DPP XOR-reduction inside each 16-lane row (result valid in every lane of the row).
+__device__ __forceinline__ uint32_t row_xor_reduce(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xF, 0xF, false);  // row_ror:4
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  return v;
+}
+
+// W4: dwordx4 loads, 4 frames per wave (16 lanes per frame), 4 chains per lane.
+// Slot s = 4*l + b (l = lane&15, b = word in the dwordx4).  Nibble tables column
+// c(s) = (s>>1) + 32*(s&1); odd frame-groups multiply chain (i+2)&3 in step i so the
+// 32 lanes of an LDS group always touch 32 distinct banks.
+template <int J, int MODE>
+__global__ __launch_bounds__(1024) void w4_kernel(const uint8_t* __restrict__ base, size_t stride, int n,
+    int nframes, const uint32_t* __restrict__ gch, const uint32_t* __restrict__ gnb, uint32_t G,
+    uint32_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  uint32_t* l32 = (uint32_t*)lds;
+  for (int i = threadIdx.x; i < 32768; i += blockDim.x) {
+    int k = i >> 13, e = (i >> 5) & 255;
+    l32[i] = gch[k * 256 + e];
+  }
+  for (int i = threadIdx.x; i < 8192; i += blockDim.x) {
+    int c = i & 63, ke = i >> 6;
+    int slot = ((c & 31) << 1) | (c >> 5);
+    l32[32768 + i] = gnb[slot * 128 + ke];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 15;
+  const int grp = lane >> 4;
+  const uint32_t c4 = (lane & 31) * 4;
+  const int pad = J * 256 - n;
+  const int W = gridDim.x * (blockDim.x >> 6);
+  const int w0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const bool odd = grp & 1;
+  // nibble column base per chain-step i: slot = 4*col + ((i + (odd?2:0)) & 3)
+  uint32_t nb[4];
+  #pragma unroll
+  for (int i = 0; i < 4; i++) {
+    int s = 4 * col + ((i + (odd ? 2 : 0)) & 3);
+    int c = (s >> 1) + 32 * (s & 1);
+    nb[i] = 131072u + c * 4u;
+  }
+
+  auto load = [&](int wf, uint4 (&x)[J]) {
+    int f = min(wf * 4 + grp, nframes - 1);
+    const uint8_t* fb = base + (size_t)f * stride;
+    #pragma unroll
+    for (int j = 0; j < J; j++) {
+      int off = 256 * j + 16 * col - pad;
+      if (j == 0) {
+        uint32_t w[4];
+        #pragma unroll
+        for (int b = 0; b < 4; b++) {
+          int o = off + 4 * b;
+          uint32_t v = *(const uint32_t*)(fb + max(o, 0));
+          const uint32_t m = (uint32_t)((o >> 31) ^ 0xFFFFFFFF) & 0xFFFFFFFFu;  // ~0 if o >= 0
+          w[b] = (v & ((o >= 0) ? 0xFFFFFFFFu : 0u)) | ((o == -4) ? G : 0u);
+          (void)m;
+        }
+        x[j] = make_uint4(w[0], w[1], w[2], w[3]);
+      } else {
+        x[j] = *(const uint4*)(fb + off);
+      }
+    }
+  };
+  auto compute = [&](int wf, const uint4 (&x)[J]) {
+    if (MODE == 1) {  // loads only
+      uint32_t a = 0;
+      #pragma unroll
+      for (int j = 0; j < J; j++) a ^= x[j].x ^ x[j].y ^ x[j].z ^ x[j].w;
+      a = row_xor_reduce(a);
+      int f = wf * 4 + grp;
+      if (col == 0 && f < nframes) out[f] = ~a;
+      return;
+    }
+    uint32_t V0 = x[0].x, V1 = x[0].y, V2 = x[0].z, V3 = x[0].w;
+    #pragma unroll
+    for (int j = 1; j < J; j++) {
+      V0 = chain(lds, V0, c4) ^ x[j].x;
+      V1 = chain(lds, V1, c4) ^ x[j].y;
+      V2 = chain(lds, V2, c4) ^ x[j].z;
+      V3 = chain(lds, V3, c4) ^ x[j].w;
+    }
+    uint32_t X0 = odd ? V2 : V0, X1 = odd ? V3 : V1, X2 = odd ? V0 : V2, X3 = odd ? V1 : V3;
+    uint32_t acc = nibmul<64>(lds, X0, nb[0]) ^ nibmul<64>(lds, X1, nb[1]) ^
+                   nibmul<64>(lds, X2, nb[2]) ^ nibmul<64>(lds, X3, nb[3]);
+    acc = row_xor_reduce(acc);
+    int f = wf * 4 + grp;
+    if (col == 0 && f < nframes) out[f] = ~acc;
+  };
+  uint4 A[J], B[J];
+  int wf = w0;
+  load(wf, A);
+  if (MODE == 2) {
+    #pragma unroll
+    for (int j = 0; j < J; j++) B[j] = make_uint4(A[j].y, A[j].z, A[j].w, A[j].x ^ wf);
+  }
+  for (; wf * 4 < nframes; wf += 2 * W) {
+    if (MODE != 2) load(wf + W, B);
+    compute(wf, A);
+    if ((wf + W) * 4 >= nframes) break;
+    if (MODE != 2) load(wf + 2 * W, A);
+    compute(wf + W, B);
+    if (MODE == 2) {
+      #pragma unroll
+      for (int j = 0; j < J; j++) { A[j].x ^= wf; B[j].y += 1; }
+    }
+  }
+}
+
+// W2: dwordx2 loads, 2 frames per wave (32 lanes per frame), explicit A/B double buffer.
+template <int J>
+__global__ __launch_bounds__(1024) void w2_kernel(const uint8_t* __restrict__ base, size_t stride, int n,
+    int nframes, const uint32_t* __restrict__ gch, const uint32_t* __restrict__ gnb, uint32_t G,
+    uint32_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  uint32_t* l32 = (uint32_t*)lds;
+  for (int i = threadIdx.x; i < 32768; i += blockDim.x) {
+    int k = i >> 13, e = (i >> 5) & 255;
+    l32[i] = gch[k * 256 + e];
+  }
+  for (int i = threadIdx.x; i < 8192; i += blockDim.x) {
+    int b = i >> 12, c = i & 31, ke = (i >> 5) & 127;
+    l32[32768 + i] = gnb[(2 * c + b) * 128 + ke];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int col = lane & 31;
+  const int grp = lane >> 5;
+  const uint32_t c4 = (lane & 31) * 4;
+  const int pad = J * 256 - n;
+  const int W = gridDim.x * (blockDim.x >> 6);
+  const int w0 = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  auto load = [&](int wf, uint2 (&x)[J]) {
+    int f = min(wf * 2 + grp, nframes - 1);
+    const uint8_t* fb = base + (size_t)f * stride;
+    #pragma unroll
+    for (int j = 0; j < J; j++) {
+      int off = 256 * j + 8 * col - pad;
+      if (j == 0) {
+        uint32_t w[2];
+        #pragma unroll
+        for (int b = 0; b < 2; b++) {
+          int o = off + 4 * b;
+          uint32_t v = *(const uint32_t*)(fb + max(o, 0));
+          const uint32_t m = (uint32_t)((o >> 31) ^ 0xFFFFFFFF) & 0xFFFFFFFFu;  // ~0 if o >= 0
+          w[b] = (v & ((o >= 0) ? 0xFFFFFFFFu : 0u)) | ((o == -4) ? G : 0u);
+          (void)m;
+        }
+        x[j] = make_uint2(w[0], w[1]);
+      } else {
+        x[j] = *(const uint2*)(fb + off);
+      }
+    }
+  };
+  auto compute = [&](int wf, const uint2 (&x)[J]) {
+    uint32_t V0 = x[0].x, V1 = x[0].y;
+    #pragma unroll
+    for (int j = 1; j < J; j++) {
+      V0 = chain(lds, V0, c4) ^ x[j].x;
+      V1 = chain(lds, V1, c4) ^ x[j].y;
+    }
+    uint32_t acc = nibmul<32>(lds, V0, 131072u + col * 4u) ^ nibmul<32>(lds, V1, 131072u + 16384u + col * 4u);
+    acc = row_xor_reduce(acc);
+    uint32_t r0 = __builtin_amdgcn_readlane(acc, 0) ^ __builtin_amdgcn_readlane(acc, 16);
+    uint32_t r1 = __builtin_amdgcn_readlane(acc, 32) ^ __builtin_amdgcn_readlane(acc, 48);
+    int f = wf * 2;
+    if (lane == 0 && f < nframes) out[f] = ~r0;
+    if (lane == 32 && f + 1 < nframes) out[f + 1] = ~r1;
+  };
+  uint2 A[J], B[J];
+  int wf = w0;
+  load(wf, A);
+  for (; wf * 2 < nframes; wf += 2 * W) {
+    load(wf + W, B);
+    compute(wf, A);
+    if ((wf + W) * 2 >= nframes) break;
+    load(wf + 2 * W, A);
+    compute(wf + W, B);
+  }
+}
+
+int main(int argc, char** argv) {
+  build_tables();
+  const int N = argc > 1 ? atoi(argv[1]) : 1000000;
+  const size_t STRIDE = 1500;
+  const int NCRC = 1496;
+  const size_t bytes = (size_t)N * STRIDE + 4096;
+  uint8_t* d; CK(hipMalloc(&d, bytes));
+  fill_kernel<<<4096, 256>>>((uint64_t*)d, bytes / 8, 0x5EED0001); CK(hipGetLastError());
+  const size_t OUTN = (size_t)N + (1 << 22);
+  uint32_t* dout; CK(hipMalloc(&dout, sizeof(uint32_t) * OUTN));
+
+  // tables
+  std::vector<uint32_t> ch(1024), nb(64 * 128);
+  for (int k = 0; k < 4; k++) for (int e = 0; e < 256; e++) ch[k * 256 + e] = adv((uint32_t)e << (8 * k), 256);
+  for (int s = 0; s < 64; s++) for (int k = 0; k < 8; k++) for (int e = 0; e < 16; e++)
+    nb[s * 128 + k * 16 + e] = adv((uint32_t)e << (4 * k), 4 * (64 - s));
+  // G = A^-4(~0): find by solving; brute force over a 32x32 GF(2) system
+  uint32_t cols[32]; for (int i = 0; i < 32; i++) cols[i] = adv(1u << i, 4);
+  uint32_t rows[32]; uint32_t rhs = 0xFFFFFFFFu;  // rows[i] = bit i of each column
+  for (int i = 0; i < 32; i++) { rows[i] = 0; for (int j = 0; j < 32; j++) rows[i] |= ((cols[j] >> i) & 1u) << j; }
+  uint32_t rb = rhs; int r = 0; int pivc[32];
+  for (int c = 0; c < 32; c++) {
+    int p = -1; for (int i = r; i < 32; i++) if ((rows[i] >> c) & 1) { p = i; break; }
+    if (p < 0) { fprintf(stderr, "singular\n"); return 1; }
+    std::swap(rows[r], rows[p]);
+    uint32_t br = (rb >> r) & 1, bp = (rb >> p) & 1; rb = (rb & ~((1u << r) | (1u << p))) | (bp << r) | (br << p);
+    for (int i = 0; i < 32; i++) if (i != r && ((rows[i] >> c) & 1)) { rows[i] ^= rows[r]; rb ^= ((rb >> r) & 1u) << i; }
+    pivc[r] = c; r++;
+  }
+  uint32_t G = 0; for (int i = 0; i < 32; i++) G |= ((rb >> i) & 1u) << pivc[i];
+  printf("G=%08X adv4(G)=%08X\n", G, adv(G, 4));
+  uint32_t *dch, *dnb; CK(hipMalloc(&dch, 4096)); CK(hipMalloc(&dnb, nb.size() * 4));
+  CK(hipMemcpy(dch, ch.data(), 4096, hipMemcpyHostToDevice));
+  CK(hipMemcpy(dnb, nb.data(), nb.size() * 4, hipMemcpyHostToDevice));
+
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  auto timeit = [&](const char* name, double algo_bytes, auto launch) {
+    launch(); CK(hipGetLastError()); CK(hipDeviceSynchronize());
+    std::vector<float> ts;
+    for (int rep = 0; rep < 20; rep++) {
+      CK(hipEventRecord(e0)); launch(); CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    float med = ts[ts.size() / 2];
+    printf("%-44s median %8.3f ms  min %8.3f ms  %8.1f GB/s (%.3f of 8 TB/s)\n", name, med, ts[0],
+           algo_bytes / med / 1e6, algo_bytes / med / 1e6 / 8000.0);
+    fflush(stdout);
+  };
+  const double fb = (double)N * STRIDE;
+  size_t nb_total = (size_t)N * STRIDE;
+  for (int g : {2048}) {
+    char nm[64];
+    snprintf(nm, 64, "coalesced dwordx4 grid=%d", g);
+    timeit(nm, fb, [&] { m_coalesced<uint4><<<g, 256>>>((const uint4*)d, nb_total / 16, dout); });
+    snprintf(nm, 64, "coalesced dwordx2 grid=%d", g);
+    timeit(nm, fb, [&] { m_coalesced<uint2><<<g, 256>>>((const uint2*)d, nb_total / 8, dout); });
+    snprintf(nm, 64, "coalesced dword grid=%d", g);
+    timeit(nm, fb, [&] { m_coalesced<uint32_t><<<g, 256>>>((const uint32_t*)d, nb_total / 4, dout); });
+  }
+
+  std::vector<uint8_t> hh((size_t)4096 * STRIDE), ht((size_t)4096 * STRIDE);
+  CK(hipMemcpy(hh.data(), d, hh.size(), hipMemcpyDeviceToHost));
+  CK(hipMemcpy(ht.data(), d + (size_t)(N - 4096) * STRIDE, ht.size(), hipMemcpyDeviceToHost));
+  std::vector<uint32_t> hout(N);
+  auto check = [&](const char* name) {
+    CK(hipMemcpy(hout.data(), dout, (size_t)N * 4, hipMemcpyDeviceToHost));
+    int bad = 0;
+    for (int f = 0; f < 4096; f++) {
+      if (hout[f] != crc_cpu(&hh[(size_t)f * STRIDE], NCRC)) bad++;
+      if (hout[N - 4096 + f] != crc_cpu(&ht[(size_t)f * STRIDE], NCRC)) bad++;
+    }
+    printf("  check %s: %d/8192 mismatches\n", name, bad); fflush(stdout);
+  };
+  const int LDSB = 131072 + 32768;
+  CK(hipFuncSetAttribute((const void*)w4_kernel<6, 0>, hipFuncAttributeMaxDynamicSharedMemorySize, LDSB));
+  CK(hipFuncSetAttribute((const void*)w4_kernel<6, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, LDSB));
+  CK(hipFuncSetAttribute((const void*)w4_kernel<6, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, LDSB));
+  for (int rep = 0; rep < 2; rep++) {
+    CK(hipMemset(dout, 0, (size_t)N * 4));
+    timeit("W4 full", fb, [&] { w4_kernel<6, 0><<<256, 1024, LDSB>>>(d, STRIDE, NCRC, N, dch, dnb, G, dout); });
+    check("W4 full");
+    timeit("W4 loads only", fb, [&] { w4_kernel<6, 1><<<256, 1024, LDSB>>>(d, STRIDE, NCRC, N, dch, dnb, G, dout); });
+    timeit("W4 compute only", fb, [&] { w4_kernel<6, 2><<<256, 1024, LDSB>>>(d, STRIDE, NCRC, N, dch, dnb, G, dout); });
+  }
+  printf("done\n");
+  return 0;
+}

@@ -1,0 +1,52 @@
+"""In-tree build of the native library (libuflowcrc.so) and of the CPU oracle.
+
+The library is compiled for gfx950 only (MI355X): hipcc --offload-arch=gfx950.  The .so lands
+next to this file so that it travels with the repository snapshot to the GPU box.
+"""
+import os
+import subprocess
+import sys
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "libuflowcrc.so")
+SOURCES = ["frame_crc.hip", "ufc_api.cpp", "crc_math.cpp"]
+HEADERS = ["frame_crc_kernels.hpp", "crc_math.hpp"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build_native(force=False, verbose=False):
+    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    deps.append(os.path.join(REPO_DIR, "include", "uflow_frame_crc.h"))
+    if not force and not _stale(LIB_PATH, deps):
+        return LIB_PATH
+    cmd = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17", "-Wall",
+           "-o", LIB_PATH + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LIB_PATH + ".tmp", LIB_PATH)
+    return LIB_PATH
+
+
+def build_oracle(force=False):
+    odir = os.path.join(REPO_DIR, "oracle")
+    target = os.path.join(odir, "liboracle.so")
+    src = os.path.join(odir, "crc_oracle.c")
+    if force or _stale(target, [src]):
+        subprocess.run(["make", "-C", odir, "-s"], check=True)
+    return target
+
+
+if __name__ == "__main__":
+    build_native(force="--force" in sys.argv, verbose=True)
+    build_oracle(force="--force" in sys.argv)
+    print(LIB_PATH)

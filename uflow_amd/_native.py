@@ -1,0 +1,72 @@
+"""ctypes binding of libuflowcrc.so (the C ABI in include/uflow_frame_crc.h).
+
+This is the Python-side equivalent of the `extern "C"` block a Rust caller would declare
+(see INTEGRATION.md).  Loading fails loudly when the in-tree library is missing: there is no
+CPU fallback for the batched entry points.
+"""
+import ctypes
+import os
+
+from ._build import LIB_PATH
+
+UFC_OK = 0
+UFC_ERR_INVALID_ARG = -1
+UFC_ERR_NO_DEVICE = -2
+UFC_ERR_HIP = -3
+UFC_ERR_NOMEM = -4
+
+# Every symbol the header declares, with its ctypes signature.
+_c_u8p = ctypes.POINTER(ctypes.c_uint8)
+_SIGNATURES = {
+    "ufc_crc32_compute": (ctypes.c_uint32, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ufc_crc32_extend": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    "ufc_frame_validate": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ufc_frame_seal": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+    "ufc_device_count": (ctypes.c_int, []),
+    "ufc_ctx_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
+    "ufc_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_error_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "ufc_ctx_last_hip_error": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_crc_batch_fixed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                           ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "ufc_crc_batch_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "ufc_seal_batch_fixed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                            ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    "ufc_seal_batch_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                             ctypes.c_void_p, ctypes.c_void_p]),
+    "ufc_validate_host_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                ctypes.c_void_p, ctypes.c_void_p]),
+}
+SYMBOLS = tuple(_SIGNATURES)
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    def __init__(self, code, what=""):
+        msg = _lib.ufc_error_string(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: {msg} (code {code})" if what else f"{msg} (code {code})")
+        self.code = code
+
+
+def lib():
+    """The loaded library (raises if libuflowcrc.so has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"libuflowcrc.so not found at {LIB_PATH}: run `python -m uflow_amd._build` "
+                              "(the native library is required; there is no CPU fallback)")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGNATURES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != UFC_OK:
+        raise NativeError(rc, what)
+    return rc

@@ -1,0 +1,118 @@
+"""Batched, device-resident frame CRC on MI355X (the hot path).
+
+`FrameCrcEngine` owns one libuflowcrc context per device and wraps the batched C-ABI entry
+points on torch tensors (torch provides device memory and the current HIP stream only).
+Per frame i:  crc[i] = compute(frame_i[:-4]),  valid[i] = len_i >= 5 and crc[i] == BE32(frame_i[-4:])
+-- the CRC gate of Frame::read (src/frame/serial/mod.rs:675-690) -- and seal writes the trailer
+(src/frame/serial/mod.rs:463-470, build.rs:151-159).
+
+CRC words are returned as int32 tensors holding the uint32 bit patterns
+(`crc.cpu().numpy().view(numpy.uint32)`).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from ._native import lib, check
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class FrameCrcEngine:
+    def __init__(self, device=None):
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        self._ctx = ctypes.c_void_p()
+        check(lib().ufc_ctx_create(ctypes.byref(self._ctx), self.device.index or 0), "ufc_ctx_create")
+
+    def close(self):
+        if self._ctx:
+            lib().ufc_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _stream(self, stream):
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def _check_dev(self, *ts):
+        for t in ts:
+            if t is not None and (t.device != self.device or not t.is_contiguous()):
+                raise ValueError(f"tensor must be contiguous on {self.device}")
+
+    # ---- fixed-stride batches ----
+    def crc_fixed(self, frames, frame_len, stride=None, n=None, crc_out=None, valid_out=None,
+                  want_crc=True, want_valid=True, stream=None):
+        """frames: uint8 tensor; frame i at byte i*stride (stride defaults to frame_len)."""
+        stride = frame_len if stride is None else stride
+        if n is None:
+            n = (frames.numel() - frame_len) // stride + 1 if frames.numel() >= frame_len else 0
+        if crc_out is None and want_crc:
+            crc_out = torch.empty(n, dtype=torch.int32, device=self.device)
+        if valid_out is None and want_valid:
+            valid_out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self._check_dev(frames, crc_out, valid_out)
+        if n and (n - 1) * stride + frame_len > frames.numel():
+            raise ValueError("frames tensor too small for n frames")
+        check(lib().ufc_crc_batch_fixed(self._ctx, _ptr(frames), stride, frame_len, n, _ptr(crc_out),
+                                        _ptr(valid_out), self._stream(stream)), "ufc_crc_batch_fixed")
+        return crc_out, valid_out
+
+    def seal_fixed(self, frames, frame_len, stride=None, n=None, crc_out=None, stream=None):
+        stride = frame_len if stride is None else stride
+        if n is None:
+            n = (frames.numel() - frame_len) // stride + 1 if frames.numel() >= frame_len else 0
+        self._check_dev(frames, crc_out)
+        if n and (n - 1) * stride + frame_len > frames.numel():
+            raise ValueError("frames tensor too small for n frames")
+        check(lib().ufc_seal_batch_fixed(self._ctx, _ptr(frames), stride, frame_len, n, _ptr(crc_out),
+                                         self._stream(stream)), "ufc_seal_batch_fixed")
+        return crc_out
+
+    # ---- variable-length (CSR) batches ----
+    def crc_varlen(self, data, offsets, crc_out=None, valid_out=None, want_crc=True, want_valid=True,
+                   stream=None):
+        """data: uint8 tensor; offsets: int64 tensor of n+1 nondecreasing byte offsets."""
+        n = offsets.numel() - 1
+        if crc_out is None and want_crc:
+            crc_out = torch.empty(max(n, 0), dtype=torch.int32, device=self.device)
+        if valid_out is None and want_valid:
+            valid_out = torch.empty(max(n, 0), dtype=torch.uint8, device=self.device)
+        if offsets.dtype != torch.int64:
+            raise ValueError("offsets must be int64")
+        self._check_dev(data, offsets, crc_out, valid_out)
+        check(lib().ufc_crc_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(crc_out), _ptr(valid_out),
+                                         self._stream(stream)), "ufc_crc_batch_varlen")
+        return crc_out, valid_out
+
+    def seal_varlen(self, data, offsets, crc_out=None, stream=None):
+        n = offsets.numel() - 1
+        if offsets.dtype != torch.int64:
+            raise ValueError("offsets must be int64")
+        self._check_dev(data, offsets, crc_out)
+        check(lib().ufc_seal_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(crc_out),
+                                          self._stream(stream)), "ufc_seal_batch_varlen")
+        return crc_out
+
+    # ---- host buffers (frames received into host memory) ----
+    def validate_host_varlen(self, data: np.ndarray, offsets: np.ndarray):
+        """numpy uint8 bytes + uint64/int64 offsets in host memory -> (crc uint32[n], valid uint8[n])."""
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        crc = np.empty(max(n, 0), dtype=np.uint32)
+        valid = np.empty(max(n, 0), dtype=np.uint8)
+        check(lib().ufc_validate_host_varlen(self._ctx, data.ctypes.data_as(ctypes.c_void_p),
+                                             offsets.ctypes.data_as(ctypes.c_void_p), n,
+                                             crc.ctypes.data_as(ctypes.c_void_p),
+                                             valid.ctypes.data_as(ctypes.c_void_p)), "ufc_validate_host_varlen")
+        return crc, valid

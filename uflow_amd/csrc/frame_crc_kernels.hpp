@@ -1,0 +1,32 @@
+// frame_crc_kernels.hpp -- interface between the C-ABI layer and the HIP kernels.
+#pragma once
+#include <cstdint>
+
+namespace ufc_dev {
+
+constexpr int kModeVarlen = 1;  // frames from a CSR offsets array
+constexpr int kModeSeal = 2;    // write the BE32 trailer instead of validating it
+constexpr int kModeFreeze = 4;  // fixed-length frames whose block count is not a multiple of JC
+
+constexpr int kBlockThreads = 1024;          // one workgroup per CU, 16 waves
+constexpr int kLdsBytes = 131072 + 32768;    // chain tables + nibble tables
+constexpr int kFramesPerBlockIter = 64;      // 16 waves x 4 frames
+
+struct KernelParams {
+  const uint8_t* bytes;       // batch base (fixed) or CSR byte buffer (varlen)
+  uint8_t* wbytes;            // same buffer, writable (seal only)
+  const uint64_t* offsets;    // varlen: n+1 offsets
+  uint64_t stride;            // fixed: bytes between frame starts
+  uint64_t frame_len;         // fixed: frame length
+  uint64_t nframes;
+  uint32_t* crc_out;          // nullable
+  uint8_t* valid_out;         // nullable (validate mode)
+  const uint32_t* chain_tab;  // device: 1024 words (A^256 byte tables)
+  const uint32_t* nib_img;    // device: 8192 words (per-slot nibble tables, LDS image)
+  uint32_t G;                 // A^-4(~0)
+};
+
+// Kernel entry for (JC blocks per chunk, mode); nullptr if not instantiated.
+const void* kernel_symbol(int jc, int mode);
+
+}  // namespace ufc_dev

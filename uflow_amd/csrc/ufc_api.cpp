@@ -1,0 +1,360 @@
+// ufc_api.cpp -- C ABI of libuflowcrc.so (declared in include/uflow_frame_crc.h).
+// Scalar host entry points mirror src/frame/serial/crc.rs:94-104 and the CRC gate / seal of
+// src/frame/serial/mod.rs:463-470, 675-690; batched entry points launch the gfx950 kernels of
+// frame_crc.hip.  Batched calls never fall back to the CPU.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/uflow_frame_crc.h"
+#include "crc_math.hpp"
+#include "frame_crc_kernels.hpp"
+
+struct ufc_ctx {
+  int device = -1;
+  int ncu = 0;
+  uint32_t* d_chain = nullptr;
+  uint32_t* d_nib = nullptr;
+  uint32_t G = 0;
+  int last_hip_error = 0;
+  // host-buffer path (ufc_validate_host_varlen): device staging, reused across calls
+  uint8_t* d_stage = nullptr;
+  size_t d_stage_cap = 0;
+  uint64_t* d_off = nullptr;
+  size_t d_off_cap = 0;  // entries
+  uint32_t* d_crc = nullptr;
+  uint8_t* d_valid = nullptr;
+  size_t d_out_cap = 0;  // frames
+  uint64_t* h_off_pinned = nullptr;
+  size_t h_off_cap = 0;
+  hipStream_t streams[2] = {nullptr, nullptr};
+};
+
+namespace {
+
+struct DeviceGuard {  // restores the caller's current device
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int hip_fail(ufc_ctx* ctx, hipError_t e) {
+  if (ctx) ctx->last_hip_error = (int)e;
+  return UFC_ERR_HIP;
+}
+
+int launch(ufc_ctx* ctx, int jc, int mode, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  const void* fn = ufc_dev::kernel_symbol(jc, mode);
+  if (!fn) return UFC_ERR_INVALID_ARG;
+  const uint64_t nsets = (kp.nframes + 3) / 4;
+  const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
+  uint64_t blocks = (nsets + waves_per_block - 1) / waves_per_block;
+  if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
+  if (blocks < 1) blocks = 1;
+  kp.chain_tab = ctx->d_chain;
+  kp.nib_img = ctx->d_nib;
+  kp.G = ctx->G;
+  void* args[] = {&kp};
+  hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args,
+                                 (size_t)ufc_dev::kLdsBytes, stream);
+  if (e != hipSuccess) return hip_fail(ctx, e);
+  return UFC_OK;
+}
+
+// Blocks-per-chunk and mode bits for a fixed frame length.
+void fixed_geometry(uint64_t frame_len, int* jc, int* freeze) {
+  const uint64_t n = frame_len >= 4 ? frame_len - 4 : frame_len;
+  const uint64_t J = (n + 4 + 255) / 256;
+  if (J <= 6) {
+    *jc = (int)J;
+    *freeze = 0;
+  } else {  // long frames: chunks of 4 blocks
+    *jc = 4;
+    *freeze = (J % 4) ? ufc_dev::kModeFreeze : 0;
+  }
+}
+
+constexpr uint64_t kMaxFrameLen = (uint64_t)1 << 30;  // per-frame limit of the 32-bit offsets math
+
+}  // namespace
+
+extern "C" {
+
+uint32_t ufc_crc32_compute(const uint8_t* data, size_t len) {
+  if (!data) return 0;
+  return ufc::host_extend(0u, data, len);
+}
+
+uint32_t ufc_crc32_extend(uint32_t initial_crc, const uint8_t* data, size_t len) {
+  if (!data) return initial_crc;
+  return ufc::host_extend(initial_crc, data, len);
+}
+
+int ufc_frame_validate(const uint8_t* frame, size_t len) {
+  if (!frame || len < 5) return 0;
+  const uint32_t c = ufc::host_extend(0u, frame, len - 4);
+  const uint8_t* t = frame + len - 4;
+  const uint32_t rx = ((uint32_t)t[0] << 24) | ((uint32_t)t[1] << 16) | ((uint32_t)t[2] << 8) | (uint32_t)t[3];
+  return c == rx ? 1 : 0;
+}
+
+int ufc_frame_seal(uint8_t* frame, size_t len) {
+  if (!frame || len < 4) return UFC_ERR_INVALID_ARG;
+  const uint32_t c = ufc::host_extend(0u, frame, len - 4);
+  uint8_t* t = frame + len - 4;
+  t[0] = (uint8_t)(c >> 24);
+  t[1] = (uint8_t)(c >> 16);
+  t[2] = (uint8_t)(c >> 8);
+  t[3] = (uint8_t)c;
+  return UFC_OK;
+}
+
+int ufc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+const char* ufc_error_string(int code) {
+  switch (code) {
+    case UFC_OK: return "ok";
+    case UFC_ERR_INVALID_ARG: return "invalid argument";
+    case UFC_ERR_NO_DEVICE: return "no usable gfx950 (MI355X) device";
+    case UFC_ERR_HIP: return "HIP runtime error (see ufc_ctx_last_hip_error)";
+    case UFC_ERR_NOMEM: return "out of memory";
+    default: return "unknown error";
+  }
+}
+
+int ufc_ctx_last_hip_error(const ufc_ctx* ctx) { return ctx ? ctx->last_hip_error : 0; }
+
+int ufc_ctx_create(ufc_ctx** out, int device) {
+  if (!out) return UFC_ERR_INVALID_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return UFC_ERR_NO_DEVICE;
+  if (device < 0 || device >= ndev) return UFC_ERR_INVALID_ARG;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return UFC_ERR_NO_DEVICE;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return UFC_ERR_NO_DEVICE;
+  DeviceGuard g(device);
+  ufc_ctx* ctx = new (std::nothrow) ufc_ctx();
+  if (!ctx) return UFC_ERR_NOMEM;
+  ctx->device = device;
+  ctx->ncu = prop.multiProcessorCount;
+  std::vector<uint32_t> chain(1024), nib(8192);
+  ufc::build_chain_table(chain.data());
+  ufc::build_nibble_image(nib.data());
+  ctx->G = ufc::init_prefix_word();
+  hipError_t e;
+  if ((e = hipMalloc(&ctx->d_chain, chain.size() * 4)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_nib, nib.size() * 4)) != hipSuccess ||
+      (e = hipMemcpy(ctx->d_chain, chain.data(), chain.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(ctx->d_nib, nib.data(), nib.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+    ufc_ctx_destroy(ctx);
+    return UFC_ERR_HIP;
+  }
+  for (int jc : {1, 2, 3, 4, 5, 6})
+    for (int mode : {0, ufc_dev::kModeSeal, ufc_dev::kModeVarlen, ufc_dev::kModeVarlen | ufc_dev::kModeSeal,
+                     ufc_dev::kModeFreeze, ufc_dev::kModeFreeze | ufc_dev::kModeSeal}) {
+      e = hipFuncSetAttribute(ufc_dev::kernel_symbol(jc, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              ufc_dev::kLdsBytes);
+      if (e != hipSuccess) {
+        ufc_ctx_destroy(ctx);
+        return UFC_ERR_HIP;
+      }
+    }
+  *out = ctx;
+  return UFC_OK;
+}
+
+int ufc_ctx_destroy(ufc_ctx* ctx) {
+  if (!ctx) return UFC_OK;
+  {
+    DeviceGuard g(ctx->device >= 0 ? ctx->device : 0);
+    if (ctx->d_chain) (void)hipFree(ctx->d_chain);
+    if (ctx->d_nib) (void)hipFree(ctx->d_nib);
+    if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    if (ctx->d_off) (void)hipFree(ctx->d_off);
+    if (ctx->d_crc) (void)hipFree(ctx->d_crc);
+    if (ctx->d_valid) (void)hipFree(ctx->d_valid);
+    if (ctx->h_off_pinned) (void)hipHostFree(ctx->h_off_pinned);
+    for (hipStream_t& s : ctx->streams)
+      if (s) (void)hipStreamDestroy(s);
+  }
+  delete ctx;
+  return UFC_OK;
+}
+
+int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
+                        uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!d_frames || stride < frame_len || frame_len > kMaxFrameLen || (!d_crc_out && !d_valid_out))
+    return UFC_ERR_INVALID_ARG;
+  int jc, freeze;
+  fixed_geometry(frame_len, &jc, &freeze);
+  ufc_dev::KernelParams kp{};
+  kp.bytes = d_frames;
+  kp.stride = stride;
+  kp.frame_len = frame_len;
+  kp.nframes = n;
+  kp.crc_out = d_crc_out;
+  kp.valid_out = d_valid_out;
+  DeviceGuard g(ctx->device);
+  return launch(ctx, jc, freeze, kp, (hipStream_t)stream);
+}
+
+int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
+                         uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!d_bytes || !d_offsets || (!d_crc_out && !d_valid_out)) return UFC_ERR_INVALID_ARG;
+  ufc_dev::KernelParams kp{};
+  kp.bytes = d_bytes;
+  kp.offsets = d_offsets;
+  kp.nframes = n;
+  kp.crc_out = d_crc_out;
+  kp.valid_out = d_valid_out;
+  DeviceGuard g(ctx->device);
+  return launch(ctx, 6, ufc_dev::kModeVarlen, kp, (hipStream_t)stream);
+}
+
+int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
+                         uint32_t* d_crc_out, void* stream) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!d_frames || stride < frame_len || frame_len < 4 || frame_len > kMaxFrameLen) return UFC_ERR_INVALID_ARG;
+  int jc, freeze;
+  fixed_geometry(frame_len, &jc, &freeze);
+  ufc_dev::KernelParams kp{};
+  kp.bytes = d_frames;
+  kp.wbytes = d_frames;
+  kp.stride = stride;
+  kp.frame_len = frame_len;
+  kp.nframes = n;
+  kp.crc_out = d_crc_out;
+  DeviceGuard g(ctx->device);
+  return launch(ctx, jc, freeze | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
+}
+
+int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
+                          uint32_t* d_crc_out, void* stream) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!d_bytes || !d_offsets) return UFC_ERR_INVALID_ARG;
+  ufc_dev::KernelParams kp{};
+  kp.bytes = d_bytes;
+  kp.wbytes = d_bytes;
+  kp.offsets = d_offsets;
+  kp.nframes = n;
+  kp.crc_out = d_crc_out;
+  DeviceGuard g(ctx->device);
+  return launch(ctx, 6, ufc_dev::kModeVarlen | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
+}
+
+int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
+                             uint32_t* h_crc_out, uint8_t* h_valid_out) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!h_bytes || !h_offsets || (!h_crc_out && !h_valid_out)) return UFC_ERR_INVALID_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (h_offsets[i + 1] < h_offsets[i]) return UFC_ERR_INVALID_ARG;
+  DeviceGuard g(ctx->device);
+  hipError_t e;
+  for (hipStream_t& s : ctx->streams)
+    if (!s && (e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return hip_fail(ctx, e);
+  // Chunking: frames are split into chunks of at most kChunkBytes of frame data (or one frame);
+  // chunk k uses staging slot k&1 on stream k&1, so H2D of chunk k+1 overlaps the CRC of chunk k.
+  const size_t kChunkBytes = (size_t)64 << 20;
+  const size_t kChunkFrames = (size_t)1 << 20;
+  const uint64_t base = h_offsets[0];
+  const uint64_t total = h_offsets[n] - base;
+  size_t max_chunk_bytes = 0, max_chunk_frames = 0;
+  std::vector<size_t> cuts;  // frame index boundaries
+  cuts.push_back(0);
+  while (cuts.back() < n) {
+    size_t a = cuts.back(), b = a + 1;
+    while (b < n && b - a < kChunkFrames && h_offsets[b + 1] - h_offsets[a] <= kChunkBytes) b++;
+    const size_t cb = (size_t)(h_offsets[b] - h_offsets[a]);
+    if (cb > max_chunk_bytes) max_chunk_bytes = cb;
+    if (b - a > max_chunk_frames) max_chunk_frames = b - a;
+    cuts.push_back(b);
+  }
+  (void)total;
+  // Grow staging (2 slots each).
+  if (ctx->d_stage_cap < 2 * max_chunk_bytes + 64) {
+    if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    ctx->d_stage = nullptr;
+    ctx->d_stage_cap = 0;
+    if ((e = hipMalloc(&ctx->d_stage, 2 * max_chunk_bytes + 64)) != hipSuccess) return hip_fail(ctx, e);
+    ctx->d_stage_cap = 2 * max_chunk_bytes + 64;
+  }
+  const size_t need_off = 2 * (max_chunk_frames + 1);
+  if (ctx->d_off_cap < need_off) {
+    if (ctx->d_off) (void)hipFree(ctx->d_off);
+    if (ctx->h_off_pinned) (void)hipHostFree(ctx->h_off_pinned);
+    ctx->d_off = nullptr;
+    ctx->h_off_pinned = nullptr;
+    ctx->d_off_cap = ctx->h_off_cap = 0;
+    if ((e = hipMalloc(&ctx->d_off, need_off * 8)) != hipSuccess) return hip_fail(ctx, e);
+    if ((e = hipHostMalloc(&ctx->h_off_pinned, need_off * 8, hipHostMallocDefault)) != hipSuccess)
+      return hip_fail(ctx, e);
+    ctx->d_off_cap = ctx->h_off_cap = need_off;
+  }
+  if (ctx->d_out_cap < 2 * max_chunk_frames) {
+    if (ctx->d_crc) (void)hipFree(ctx->d_crc);
+    if (ctx->d_valid) (void)hipFree(ctx->d_valid);
+    ctx->d_crc = nullptr;
+    ctx->d_valid = nullptr;
+    ctx->d_out_cap = 0;
+    if ((e = hipMalloc(&ctx->d_crc, 2 * max_chunk_frames * 4)) != hipSuccess) return hip_fail(ctx, e);
+    if ((e = hipMalloc(&ctx->d_valid, 2 * max_chunk_frames)) != hipSuccess) return hip_fail(ctx, e);
+    ctx->d_out_cap = 2 * max_chunk_frames;
+  }
+  for (size_t k = 0; k + 1 < cuts.size(); k++) {
+    const int slot = (int)(k & 1);
+    hipStream_t s = ctx->streams[slot];
+    const size_t a = cuts[k], b = cuts[k + 1], nf = b - a;
+    const uint64_t off0 = h_offsets[a];
+    const size_t bytes = (size_t)(h_offsets[b] - off0);
+    uint8_t* dst = ctx->d_stage + (size_t)slot * (max_chunk_bytes + 32);
+    uint64_t* hoff = ctx->h_off_pinned + (size_t)slot * (max_chunk_frames + 1);
+    uint64_t* doff = ctx->d_off + (size_t)slot * (max_chunk_frames + 1);
+    uint32_t* dcrc = ctx->d_crc + (size_t)slot * max_chunk_frames;
+    uint8_t* dval = ctx->d_valid + (size_t)slot * max_chunk_frames;
+    // the pinned offsets slot may still be in use by the H2D of chunk k-2 on the same stream
+    if (k >= 2 && (e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e);
+    for (size_t i = 0; i <= nf; i++) hoff[i] = h_offsets[a + i] - off0;
+    if (bytes && (e = hipMemcpyAsync(dst, h_bytes + off0, bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return hip_fail(ctx, e);
+    if ((e = hipMemcpyAsync(doff, hoff, (nf + 1) * 8, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e);
+    ufc_dev::KernelParams kp{};
+    kp.bytes = dst;
+    kp.offsets = doff;
+    kp.nframes = nf;
+    kp.crc_out = dcrc;
+    kp.valid_out = dval;
+    int rc = launch(ctx, 6, ufc_dev::kModeVarlen, kp, s);
+    if (rc != UFC_OK) return rc;
+    if (h_crc_out && (e = hipMemcpyAsync(h_crc_out + a, dcrc, nf * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(ctx, e);
+    if (h_valid_out && (e = hipMemcpyAsync(h_valid_out + a, dval, nf, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(ctx, e);
+  }
+  for (hipStream_t s : ctx->streams)
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e);
+  return UFC_OK;
+}
+
+}  // extern "C"
