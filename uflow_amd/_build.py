@@ -23,18 +23,22 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_native(force=False, verbose=False):
+def build_native(force=False, verbose=False, tuning=False, out=None):
+    """tuning=True adds the ablation kernels (-DUFC_TUNING) and writes to `out` instead."""
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     deps.append(os.path.join(REPO_DIR, "include", "uflow_frame_crc.h"))
-    if not force and not _stale(LIB_PATH, deps):
-        return LIB_PATH
+    target = out or LIB_PATH
+    if not force and not _stale(target, deps):
+        return target
     cmd = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17", "-Wall",
-           "-o", LIB_PATH + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+           "-o", target + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    if tuning:
+        cmd.insert(1, "-DUFC_TUNING")
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(target + ".tmp", target)
+    return target
 
 
 def build_oracle(force=False):

@@ -7,7 +7,10 @@ CPU fallback for the batched entry points.
 import ctypes
 import os
 
-from ._build import LIB_PATH
+from ._build import LIB_PATH as _DEFAULT_LIB
+
+# UFC_LIB overrides the library path (tuning builds only; the product loads the in-tree .so).
+LIB_PATH = os.environ.get("UFC_LIB", _DEFAULT_LIB)
 
 UFC_OK = 0
 UFC_ERR_INVALID_ARG = -1

@@ -22,11 +22,14 @@
 // in four independent chains.  Frames whose block count differs inside a wave (varlen) run the
 // wave's maximum and freeze their chains after their own last block.
 //
-// LDS (one 1024-thread workgroup per CU, 160 KiB):
-//   [0, 128K)    chain tables: entry e of table k, copy c at byte k*32768 + e*128 + c*4
-//   [128K,160K)  nibble tables: slot s, nibble k, value e at byte 131072 + (k*16+e)*256 + c(s)*4,
-//                c(s) = (s >> 1) + 32*(s & 1).  In nibble step i, frames in odd 16-lane groups use
-//                chain (i+2)&3, so the 32 lanes of an LDS lane-group hit 32 distinct banks.
+// LDS (one 1024-thread workgroup per CU, 160 KiB), laid out so that every table address is ONE
+// v_perm_b32 (byte select) of the value being looked up:
+//   [0, 32K)     nibble tables: slot s, nibble k, value e at byte k*4096 + e*256 + c(s)*4, with
+//                c(s) = (s >> 1) + 32*(s & 1); k*4096 goes in the ds_read offset.  In nibble step i,
+//                frames in odd 16-lane groups use chain (i+2)&3, so the 32 lanes of an LDS
+//                lane-group hit 32 distinct banks.
+//   [32K, 160K)  chain tables (two per 256-byte row): table k = 2p + t, entry e, copy c at byte
+//                32768 + p*65536 + e*256 + t*128 + c*4, c = lane & 31 (bank = c: conflict-free).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
@@ -35,30 +38,64 @@
 namespace ufc_dev {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// Global-address-space views: loads through them compile to global_load_* (vmcnt only).  Plain
+// or non-temporal loads through generic pointers can become flat_load_*, which also count in
+// lgkmcnt and make every LDS wait drain the HBM prefetch.
+typedef const __attribute__((address_space(1))) u32x4 g_u32x4;
+typedef const __attribute__((address_space(1))) uint8_t g_u8;
+typedef const __attribute__((address_space(1))) uint32_t g_u32;
+typedef const __attribute__((address_space(1))) uint64_t g_u64;
+typedef __attribute__((address_space(1))) uint8_t g_u8w;
+typedef __attribute__((address_space(1))) uint32_t g_u32w;
+
+template <typename G, typename T>
+__device__ __forceinline__ G* as_global(T* p) {
+  return (G*)(p);
+}
 
 __device__ __forceinline__ uint32_t lds_ld(const char* lds, uint32_t byteoff) {
   return *(const uint32_t*)(lds + byteoff);
 }
 
-// A^256(v) with the replicated byte tables; c4 = (lane & 31) * 4.
-__device__ __forceinline__ uint32_t chain_step(const char* lds, uint32_t v, uint32_t c4) {
-  const uint32_t a0 = ((v << 7) & 0x7F80u) | c4;
-  const uint32_t a1 = ((v >> 1) & 0x7F80u) | c4;
-  const uint32_t a2 = ((v >> 9) & 0x7F80u) | c4;
-  const uint32_t a3 = ((v >> 17) & 0x7F80u) | c4;
-  return lds_ld(lds, a0) ^ lds_ld(lds, a1 + 32768u) ^ lds_ld(lds, a2 + 65536u) ^ lds_ld(lds, a3 + 98304u);
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
 }
 
-// Multiply by the slot constant whose nibble-table column starts at byte `base`.
-__device__ __forceinline__ uint32_t nib_mul(const char* lds, uint32_t v, uint32_t base) {
-  uint32_t r = 0;
+// v_perm_b32 byte select: result byte i = byte sel.i of the 8 bytes {hi: a, lo: b};
+// selector 0..3 picks b's bytes, 4..7 a's bytes, 0x0C gives 0x00.
+__device__ __forceinline__ uint32_t perm(uint32_t a, uint32_t b, uint32_t sel) {
+  return __builtin_amdgcn_perm(a, b, sel);
+}
+
+constexpr uint32_t kChainBase = 32768u;
+// Address of table k's entry for byte k of v: bytes [c4 + 128*(k&1), v.byte_k, k>>1, 0] with
+// K = per-lane bytes [c4, c4 + 128, 0, 1]; the 32 KiB base goes in the ds_read offset.
+constexpr uint32_t kSelChain0 = 0x0C020400u, kSelChain1 = 0x0C020501u, kSelChain2 = 0x0C030600u,
+                   kSelChain3 = 0x0C030701u;
+
+// A^256(v) ^ x with the replicated byte tables: 4 v_perm + 4 ds_read_b32 + 2 v_bitop3.
+__device__ __forceinline__ uint32_t chain_step(const char* lds, uint32_t v, uint32_t K, uint32_t x) {
+  const char* t = lds + kChainBase;
+  const uint32_t r0 = *(const uint32_t*)(t + perm(v, K, kSelChain0));
+  const uint32_t r1 = *(const uint32_t*)(t + perm(v, K, kSelChain1));
+  const uint32_t r2 = *(const uint32_t*)(t + perm(v, K, kSelChain2));
+  const uint32_t r3 = *(const uint32_t*)(t + perm(v, K, kSelChain3));
+  return xor3(xor3(r0, r1, r2), r3, x);
+}
+
+// Multiply v by the constant of the slot whose column byte-offset is byte `i` of K2:
+// nibble k of v indexes row (k*16 + e); address bytes [K2.byte_i, nibble, 0, 0] + k*4096.
+template <int I>
+__device__ __forceinline__ uint32_t nib_mul(const char* lds, uint32_t v, uint32_t K2) {
+  const uint32_t lo = v & 0x0F0F0F0Fu;          // nibbles 0,2,4,6 as bytes
+  const uint32_t hi = (v >> 4) & 0x0F0F0F0Fu;   // nibbles 1,3,5,7 as bytes
+  uint32_t r[8];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
-    const int sh = 4 * k - 8;  // nibble k -> bits [8, 12) of the row offset (row stride 256 B)
-    const uint32_t e = (sh >= 0) ? (v >> sh) : (v << (-sh));
-    r ^= lds_ld(lds, (e & 0xF00u) + base + (uint32_t)(k * 4096));
+    const uint32_t sel = 0x0C0C0000u | ((uint32_t)(4 + (k >> 1)) << 8) | (uint32_t)I;
+    r[k] = *(const uint32_t*)(lds + perm((k & 1) ? hi : lo, K2, sel) + k * 4096);
   }
-  return r;
+  return xor3(xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6]), r[7], 0u);
 }
 
 // XOR over the 16 lanes of a DPP row; every lane of the row receives the total.
@@ -105,7 +142,8 @@ struct Lane {
   int col;        // lane within the frame's 16-lane group
   int grp;        // frame group 0..3 inside the wave
   bool odd;       // grp & 1
-  uint32_t c4;    // (lane & 31) * 4
+  uint32_t K;     // chain-table perm key: bytes [c4, c4 + 128, 0, 1], c4 = (lane & 31) * 4
+  uint32_t K2;    // nibble-table perm key: byte i = column*4 of the slot multiplied in nibble step i
   uint32_t G;
 };
 
@@ -126,10 +164,10 @@ __device__ __forceinline__ void process_block(const Lane& L, const FrameDesc& d,
     return;
   }
   if (blk == 1) x.x = fix_word(x.x, 256 + 16 * L.col - d.pad, L.G);
-  const uint32_t n0 = chain_step(L.lds, c.v0, L.c4) ^ x.x;
-  const uint32_t n1 = chain_step(L.lds, c.v1, L.c4) ^ x.y;
-  const uint32_t n2 = chain_step(L.lds, c.v2, L.c4) ^ x.z;
-  const uint32_t n3 = chain_step(L.lds, c.v3, L.c4) ^ x.w;
+  const uint32_t n0 = chain_step(L.lds, c.v0, L.K, x.x);
+  const uint32_t n1 = chain_step(L.lds, c.v1, L.K, x.y);
+  const uint32_t n2 = chain_step(L.lds, c.v2, L.K, x.z);
+  const uint32_t n3 = chain_step(L.lds, c.v3, L.K, x.w);
   if (FREEZE) {
     const bool act = blk < d.J;
     c.v0 = act ? n0 : c.v0;
@@ -144,50 +182,41 @@ __device__ __forceinline__ void process_block(const Lane& L, const FrameDesc& d,
 // Slot constants, 16-lane XOR, outputs of one frame set.
 template <bool SEAL>
 __device__ __forceinline__ void finish_set(const Lane& L, const KernelParams& p, uint64_t set, const FrameDesc& d,
-                                           const Chains& c) {
+                                           const Chains& c, uint32_t trailer_le) {
   const uint32_t X0 = L.odd ? c.v2 : c.v0, X1 = L.odd ? c.v3 : c.v1;
   const uint32_t X2 = L.odd ? c.v0 : c.v2, X3 = L.odd ? c.v1 : c.v3;
-  uint32_t acc = 0;
-  const uint32_t X[4] = {X0, X1, X2, X3};
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const int s = 4 * L.col + ((i + (L.odd ? 2 : 0)) & 3);
-    const uint32_t nbase = 131072u + (uint32_t)((s >> 1) + 32 * (s & 1)) * 4u;
-    acc ^= nib_mul(L.lds, X[i], nbase);
-  }
+  uint32_t acc = xor3(nib_mul<0>(L.lds, X0, L.K2), nib_mul<1>(L.lds, X1, L.K2), nib_mul<2>(L.lds, X2, L.K2)) ^
+                 nib_mul<3>(L.lds, X3, L.K2);
   acc = row_xor16(acc);
   const uint32_t crc = ~acc;
   const uint64_t f = set * 4 + (uint64_t)L.grp;
   if (L.col == 0 && f < p.nframes) {
     if (SEAL) {
       if (d.len >= 4u) {
-        uint8_t* t = p.wbytes + d.start + d.n;
+        g_u8w* t = as_global<g_u8w>(p.wbytes + d.start + d.n);
         t[0] = (uint8_t)(crc >> 24);
         t[1] = (uint8_t)(crc >> 16);
         t[2] = (uint8_t)(crc >> 8);
         t[3] = (uint8_t)crc;
       }
-      if (p.crc_out) p.crc_out[f] = crc;
+      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crc;
     } else {
-      if (p.crc_out) p.crc_out[f] = crc;
+      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crc;
       if (p.valid_out) {
         uint8_t ok = 0;
-        if (d.len >= 5u) {
-          const uint8_t* t = p.bytes + d.start + d.n;
-          const uint32_t rx = ((uint32_t)t[0] << 24) | ((uint32_t)t[1] << 16) | ((uint32_t)t[2] << 8) | (uint32_t)t[3];
-          ok = (rx == crc) ? 1 : 0;
-        }
-        p.valid_out[f] = ok;
+        if (d.len >= 5u) ok = (__builtin_bswap32(trailer_le) == crc) ? 1 : 0;
+        *as_global<g_u8w>(p.valid_out + f) = ok;
       }
     }
   }
 }
 
 // Slow path for a whole frame set (edge/tail sets: frames whose fast loads could leave the
-// buffer).  Byte loads clamped into [0, n) of the frame; one block at a time, not unrolled.
+// buffer).  Byte loads restricted to [0, n) of the frame, one block at a time, not unrolled, so
+// that it adds no register pressure to the fast path.
 template <bool FREEZE, bool SEAL>
-__device__ __noinline__ void slow_set(const Lane& L, const KernelParams& p, uint64_t set, const FrameDesc& d,
-                                      int nblocks) {
+__device__ __forceinline__ void slow_set(const Lane& L, const KernelParams& p, uint64_t set, const FrameDesc& d,
+                                         int nblocks) {
   Chains c{0u, 0u, 0u, 0u};
 #pragma unroll 1
   for (int blk = 0; blk < nblocks; blk++) {
@@ -195,58 +224,85 @@ __device__ __noinline__ void slow_set(const Lane& L, const KernelParams& p, uint
     uint32_t w[4];
 #pragma unroll
     for (int b = 0; b < 4; b++) {
+      const int o = 256 * bl + 16 * L.col + 4 * b - d.pad;
       uint32_t acc = 0;
-#pragma unroll
+#pragma unroll 1
       for (int k = 0; k < 4; k++) {
-        const int o = 256 * bl + 16 * L.col + 4 * b + k - d.pad;
-        const int oc = min(max(o, 0), max((int)d.n - 1, 0));
-        const uint32_t byte = (d.n > 0u) ? (uint32_t)p.bytes[d.start + (uint64_t)oc] : 0u;
-        acc |= ((o >= 0) ? byte : 0u) << (8 * k);
+        const int ob = o + k;
+        if (ob >= 0 && ob < (int)d.n) acc |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
       }
       w[b] = acc;
     }
     process_block<true>(L, d, blk, make_uint4(w[0], w[1], w[2], w[3]), c);
   }
-  finish_set<SEAL>(L, p, set, d, c);
+  uint32_t tr = 0;
+  if (!SEAL && d.len >= 5u) {
+    g_u8* t = as_global<g_u8>(p.bytes + d.start + d.n);
+    tr = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
+  }
+  finish_set<SEAL>(L, p, set, d, c, tr);
 }
 
-template <int JC, bool FREEZE, bool CHUNK0>
-__device__ __forceinline__ void compute_chunk(const Lane& L, const FrameDesc& d, int chunk, const uint4 (&x)[JC],
-                                              Chains& c) {
-#pragma unroll
-  for (int j = 0; j < JC; j++) process_block<FREEZE>(L, d, CHUNK0 ? j : chunk * JC + j, x[j], c);
-}
+// Fast-path item buffer: JC blocks of each of the NS frame sets of a wave-iteration, plus the
+// frames' trailer words.  The trailer word is loaded together with the data so that no load
+// is issued after the next item's prefetch (in-order vmcnt would force a wait on it).
+template <int NS, int JC>
+struct ItemBuf {
+  uint4 x[NS][JC];
+  uint32_t tr[NS];  // 4 trailer bytes (little-endian load); validate mode only
+};
 
-// Fast load of one chunk: one non-temporal dwordx4 per block at base + 256*blk (base already
-// includes 16*col - pad; block 0 may read bytes before the frame, which fix_word masks).
-template <int JC>
-__device__ __forceinline__ void load_chunk(const uint8_t* lane_base, int chunk, uint4 (&x)[JC]) {
-  const uint8_t* q = lane_base + (int64_t)chunk * (JC * 256);
+template <int NS, int JC, bool SEAL, bool NO_TRAILER = false>
+__device__ __forceinline__ void load_item(const uint8_t* const (&lane_base)[NS], const uint8_t* const (&trailer)[NS],
+                                          int chunk, ItemBuf<NS, JC>& b) {
 #pragma unroll
-  for (int j = 0; j < JC; j++) {
-    const u32x4 v = __builtin_nontemporal_load((const u32x4*)(q + 256 * j));
-    x[j] = make_uint4(v.x, v.y, v.z, v.w);
+  for (int k = 0; k < NS; k++) {
+    const uint8_t* q = lane_base[k] + (int64_t)chunk * (JC * 256);
+#pragma unroll
+    for (int j = 0; j < JC; j++) {
+      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
+      b.x[k][j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    if (!SEAL && !NO_TRAILER) b.tr[k] = *as_global<g_u32>(trailer[k]);
+    if (NO_TRAILER) b.tr[k] = 0;
   }
 }
 
-template <int JC, int MODE>
+// Blocks j of all NS sets are processed back to back (j outer, k inner): 4*NS independent
+// chains per lane hide the LDS latency of each Horner step.
+template <int NS, int JC, bool FREEZE, bool CHUNK0>
+__device__ __forceinline__ void compute_item(const Lane& L, const FrameDesc (&d)[NS], int chunk,
+                                             const ItemBuf<NS, JC>& b, Chains (&c)[NS]) {
+#pragma unroll
+  for (int j = 0; j < JC; j++)
+#pragma unroll
+    for (int k = 0; k < NS; k++) process_block<FREEZE>(L, d[k], CHUNK0 ? j : chunk * JC + j, b.x[k][j], c[k]);
+}
+
+template <int NS, int JC, int MODE>
 __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
   constexpr bool VARLEN = (MODE & kModeVarlen) != 0;
   constexpr bool SEAL = (MODE & kModeSeal) != 0;
   constexpr bool FREEZE = VARLEN || (MODE & kModeFreeze) != 0;  // blocks past J may occur in a chunk
+  constexpr bool NO_COMPUTE = (MODE & kModeAblateCompute) != 0;  // tuning builds only
+  constexpr bool NO_LOADS = (MODE & kModeAblateLoads) != 0;      // tuning builds only
+  constexpr bool NO_TRAILER = (MODE & 32) != 0;                  // tuning builds only
+  constexpr bool NO_STORES = (MODE & 64) != 0;                   // tuning builds only
+  constexpr bool NO_STAGING = (MODE & 128) != 0;                 // tuning builds only
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // ---- stage the tables into LDS: one global round trip per thread ----
-  {
+  if (!NO_STAGING) {
     const int t = threadIdx.x;  // blockDim.x == 1024 (set by the launcher)
-    const uint32_t cv = p.chain_tab[t];
-    const u32x4 n0 = *(const u32x4*)(p.nib_img + 8 * t);
-    const u32x4 n1 = *(const u32x4*)(p.nib_img + 8 * t + 4);
-    const uint32_t cbase = (uint32_t)(t >> 8) * 32768u + (uint32_t)(t & 255) * 128u;
+    const uint32_t cv = *as_global<g_u32>(p.chain_tab + t);
+    const u32x4 n0 = *as_global<g_u32x4>(p.nib_img + 8 * t);
+    const u32x4 n1 = *as_global<g_u32x4>(p.nib_img + 8 * t + 4);
+    const uint32_t k = (uint32_t)t >> 8, e = (uint32_t)t & 255u;
+    const uint32_t cbase = kChainBase + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
     const u32x4 cr = {cv, cv, cv, cv};
 #pragma unroll
     for (int i = 0; i < 8; i++) *(u32x4*)(lds + cbase + 16 * i) = cr;
-    *(u32x4*)(lds + 131072 + 32 * t) = n0;
-    *(u32x4*)(lds + 131072 + 32 * t + 16) = n1;
+    *(u32x4*)(lds + 32 * t) = n0;
+    *(u32x4*)(lds + 32 * t + 16) = n1;
   }
   __syncthreads();
 
@@ -256,170 +312,268 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
   L.col = lane & 15;
   L.grp = lane >> 4;
   L.odd = (L.grp & 1) != 0;
-  L.c4 = (uint32_t)(lane & 31) * 4u;
+  {
+    const uint32_t c4 = (uint32_t)(lane & 31) * 4u;
+    L.K = c4 | ((c4 + 128u) << 8) | (1u << 24);
+    uint32_t k2 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int s = 4 * L.col + ((i + (L.odd ? 2 : 0)) & 3);
+      k2 |= (uint32_t)(((s >> 1) + 32 * (s & 1)) * 4) << (8 * i);
+    }
+    L.K2 = k2;
+  }
   L.G = p.G;
-  const uint64_t nsets = (p.nframes + 3) >> 2;  // 4 frames per wave-iteration
+  const uint64_t nsets = (p.nframes + 3) >> 2;        // 4 frames per set (one per 16-lane group)
+  const uint64_t nsup = (nsets + NS - 1) / NS;        // NS sets per wave-iteration
   const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  uint64_t set = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (set >= nsets) return;
+  // Wave-uniform item counter, made provably uniform (SGPR) so that loop control compiles to
+  // scalar branches and no load sits behind an exec mask.
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint64_t sup = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  if (sup >= nsup) return;
   // End of the readable batch bytes (fast loads must stay below it).
-  const uint64_t buf_end = VARLEN ? p.offsets[p.nframes] : (p.nframes - 1) * p.stride + p.frame_len;
+  const uint64_t buf_end =
+      VARLEN ? *as_global<g_u64>(p.offsets + p.nframes) : (p.nframes - 1) * p.stride + p.frame_len;
 
-  auto frame_index = [&](uint64_t s) -> uint64_t {
-    const uint64_t f = s * 4 + (uint64_t)L.grp;
+  auto frame_index = [&](uint64_t set) -> uint64_t {
+    const uint64_t f = set * 4 + (uint64_t)L.grp;
     return f < p.nframes ? f : p.nframes - 1;
   };
-  auto desc_now = [&](uint64_t s) -> FrameDesc {
-    const uint64_t f = frame_index(s);
+  auto desc_now = [&](uint64_t set) -> FrameDesc {
+    const uint64_t f = frame_index(set);
     if (VARLEN) {
-      const uint64_t a = p.offsets[f], b = p.offsets[f + 1];
+      const uint64_t a = *as_global<g_u64>(p.offsets + f), b = *as_global<g_u64>(p.offsets + f + 1);
       return make_desc(a, b - a);
     }
     return make_desc(f * p.stride, p.frame_len);
   };
-  auto wave_any = [&](int v) -> bool {
-    return (__builtin_amdgcn_readlane(v, 0) | __builtin_amdgcn_readlane(v, 16) | __builtin_amdgcn_readlane(v, 32) |
-            __builtin_amdgcn_readlane(v, 48)) != 0;
+  auto wave_max = [&](int v) -> int {
+    int m = __builtin_amdgcn_readlane(v, 0);
+    m = max(m, __builtin_amdgcn_readlane(v, 16));
+    m = max(m, __builtin_amdgcn_readlane(v, 32));
+    m = max(m, __builtin_amdgcn_readlane(v, 48));
+    return m;
   };
-  auto wave_nch = [&](int J) -> int {
-    int m = __builtin_amdgcn_readlane(J, 0);
-    m = max(m, __builtin_amdgcn_readlane(J, 16));
-    m = max(m, __builtin_amdgcn_readlane(J, 32));
-    m = max(m, __builtin_amdgcn_readlane(J, 48));
-    return (m + JC - 1) / JC;
+  auto item_nch = [&](const FrameDesc (&dd)[NS]) -> int {
+    int m = 0;
+#pragma unroll
+    for (int k = 0; k < NS; k++) m = max(m, dd[k].J);
+    return (wave_max(m) + JC - 1) / JC;
   };
-  // Fast loads of the set read [start - pad, start - pad + 256*JC*nch); they must stay in the buffer.
-  auto wave_slow = [&](const FrameDesc& d, int nch) -> bool {
-    const bool bad = d.start < (uint64_t)d.pad || d.start - d.pad + (uint64_t)(256 * JC) * nch > buf_end;
-    return wave_any(bad ? 1 : 0);
+  // Fast loads read [start - pad, start - pad + 256*JC*nch) of every frame: stay in the buffer.
+  auto item_slow = [&](const FrameDesc (&dd)[NS], int nch) -> bool {
+    int bad = 0;
+#pragma unroll
+    for (int k = 0; k < NS; k++)
+      bad |= (dd[k].start < (uint64_t)dd[k].pad ||
+              dd[k].start - dd[k].pad + (uint64_t)(256 * JC) * nch > buf_end) ? 1 : 0;
+    return wave_max(bad) != 0;
+  };
+  auto trailer_ptr = [&](const FrameDesc& dd) -> const uint8_t* {
+    return p.bytes + dd.start + (dd.len >= 4u ? dd.n : 0u);  // frames without trailer: harmless address
+  };
+  auto slow_item = [&](uint64_t s, const FrameDesc (&dd)[NS], int nch) {
+#pragma unroll 1
+    for (int k = 0; k < NS; k++)
+      if (s * NS + k < nsets) slow_set<FREEZE, SEAL>(L, p, s * NS + k, dd[k], nch * JC);
   };
 
-  FrameDesc d = desc_now(set);
-  int nch = wave_nch(d.J);
-  // Edge sets (first sets of the batch) through the slow path.
-  while (wave_slow(d, nch)) {
-    slow_set<FREEZE, SEAL>(L, p, set, d, nch * JC);
-    set += W;
-    if (set >= nsets) return;
-    d = desc_now(set);
-    nch = wave_nch(d.J);
+  FrameDesc d[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) d[k] = desc_now(sup * NS + k);
+  int nch = item_nch(d);
+  // Edge items (first sets of the batch) through the slow path.
+  while (item_slow(d, nch)) {
+    slow_item(sup, d, nch);
+    sup += W;
+    if (sup >= nsup) return;
+#pragma unroll
+    for (int k = 0; k < NS; k++) d[k] = desc_now(sup * NS + k);
+    nch = item_nch(d);
   }
 
-  // Varlen: the offsets of the NEXT set are loaded one set ahead.
-  uint64_t pre_a = 0, pre_b = 0;
+  // Varlen: the offsets of the NEXT item are loaded one item ahead.
+  uint64_t pre_a[NS], pre_b[NS];
   auto prefetch_offsets = [&](uint64_t s2) {
     if (VARLEN) {
-      const uint64_t f = frame_index(s2 < nsets ? s2 : set);
-      pre_a = p.offsets[f];
-      pre_b = p.offsets[f + 1];
+#pragma unroll
+      for (int k = 0; k < NS; k++) {
+        const uint64_t f = frame_index((s2 < nsup ? s2 : sup) * NS + k);
+        pre_a[k] = *as_global<g_u64>(p.offsets + f);
+        pre_b[k] = *as_global<g_u64>(p.offsets + f + 1);
+      }
     }
   };
-  auto desc_next = [&](uint64_t s2) -> FrameDesc {
-    if (VARLEN) return make_desc(pre_a, pre_b - pre_a);
-    return make_desc(frame_index(s2) * p.stride, p.frame_len);
+  auto desc_next = [&](uint64_t s2, FrameDesc (&dd)[NS]) {
+#pragma unroll
+    for (int k = 0; k < NS; k++)
+      dd[k] = VARLEN ? make_desc(pre_a[k], pre_b[k] - pre_a[k]) : make_desc(frame_index(s2 * NS + k) * p.stride, p.frame_len);
   };
-  prefetch_offsets(set + W);
+  prefetch_offsets(sup + W);
 
-  // Main loop, double-buffered over items (set, chunk): the next item's loads are in flight
-  // while the current one is computed.  The buffers alternate explicitly (a register copy
+  // Main loop, double-buffered over items (super-set, chunk): the next item's loads are in
+  // flight while the current one is computed.  Buffers alternate explicitly (a register copy
   // would make hipcc wait for every outstanding load at the loop head).
-  Chains c{0u, 0u, 0u, 0u};
+  Chains c[NS];
   int chunk = 0;
-  const uint8_t* base_cur = p.bytes + d.start - d.pad + 16 * L.col;
-  bool go_slow = false;  // the next set needs the slow path (tail of the batch)
-  auto step = [&](uint4 (&cur)[JC], uint4 (&nxt)[JC]) -> bool {
-    uint64_t set2 = set;
+  const uint8_t* base_cur[NS];
+  const uint8_t* tr_cur[NS];
+#pragma unroll
+  for (int k = 0; k < NS; k++) {
+    base_cur[k] = p.bytes + d[k].start - d[k].pad + 16 * L.col;
+    tr_cur[k] = trailer_ptr(d[k]);
+  }
+  bool go_slow = false;  // the next item needs the slow path (tail of the batch)
+  auto step = [&](ItemBuf<NS, JC>& cur, ItemBuf<NS, JC>& nxt) -> bool {
+    uint64_t sup2 = sup;
     int chunk2 = chunk + 1, nch2 = nch;
-    FrameDesc d2 = d;
-    const uint8_t* base2 = base_cur;
-    const bool newset = (chunk2 == nch);
+    FrameDesc d2[NS];
+    const uint8_t* base2[NS];
+    const uint8_t* tr2[NS];
+#pragma unroll
+    for (int k = 0; k < NS; k++) { d2[k] = d[k]; base2[k] = base_cur[k]; tr2[k] = tr_cur[k]; }
+    const bool newitem = (chunk2 == nch);
     bool more = true;
-    if (newset) {
-      set2 = set + W;
+    if (newitem) {
+      sup2 = sup + W;
       chunk2 = 0;
-      more = set2 < nsets;
+      more = sup2 < nsup;
       if (more) {
-        d2 = desc_next(set2);
-        nch2 = wave_nch(d2.J);
-        prefetch_offsets(set2 + W);
-        if (wave_slow(d2, nch2)) {
+        desc_next(sup2, d2);
+        nch2 = item_nch(d2);
+        prefetch_offsets(sup2 + W);
+        if (item_slow(d2, nch2)) {
           go_slow = true;
           more = false;
         }
-        base2 = p.bytes + d2.start - d2.pad + 16 * L.col;
+#pragma unroll
+        for (int k = 0; k < NS; k++) {
+          base2[k] = p.bytes + d2[k].start - d2[k].pad + 16 * L.col;
+          tr2[k] = trailer_ptr(d2[k]);
+        }
       }
     }
-    if (more) load_chunk<JC>(base2, chunk2, nxt);
-    if (chunk == 0)
-      compute_chunk<JC, FREEZE, true>(L, d, 0, cur, c);
+    // Unconditional prefetch (the last one re-reads the current item): a load behind a branch
+    // makes the waitcnt pass assume it was skipped and wait for the whole prefetch.
+    {
+      const uint8_t* lb[NS];
+      const uint8_t* lt[NS];
+#pragma unroll
+      for (int k = 0; k < NS; k++) { lb[k] = more ? base2[k] : base_cur[k]; lt[k] = more ? tr2[k] : tr_cur[k]; }
+      if (NO_LOADS) {
+#pragma unroll
+        for (int k = 0; k < NS; k++)
+#pragma unroll
+          for (int j = 0; j < JC; j++) nxt.x[k][j] = make_uint4(cur.x[k][j].y, cur.x[k][j].z, cur.x[k][j].w, cur.x[k][j].x ^ chunk2);
+      } else {
+        load_item<NS, JC, SEAL, NO_TRAILER>(lb, lt, more ? chunk2 : chunk, nxt);
+      }
+    }
+    if (NO_COMPUTE) {
+#pragma unroll
+      for (int k = 0; k < NS; k++)
+#pragma unroll
+        for (int j = 0; j < JC; j++) c[k].v0 ^= cur.x[k][j].x ^ cur.x[k][j].y ^ cur.x[k][j].z ^ cur.x[k][j].w;
+    } else if (chunk == 0)
+      compute_item<NS, JC, FREEZE, true>(L, d, 0, cur, c);
     else {
       __builtin_assume(chunk >= 1);
-      compute_chunk<JC, FREEZE, false>(L, d, chunk, cur, c);
+      compute_item<NS, JC, FREEZE, false>(L, d, chunk, cur, c);
     }
-    if (newset) finish_set<SEAL>(L, p, set, d, c);
-    if (go_slow) {  // hand the tail set over to the slow loop below
-      set = set2;
-      d = d2;
+    if (newitem) {
+#pragma unroll
+      for (int k = 0; k < NS; k++) {
+        if (NO_STORES) {
+          if (c[k].v0 == 0x12345678u && c[k].v1 == cur.tr[k]) *as_global<g_u32w>(p.crc_out) = 1u;  // keep live
+        } else {
+          finish_set<SEAL>(L, p, sup * NS + k, d[k], c[k], cur.tr[k]);
+        }
+      }
+    }
+    if (go_slow) {  // hand the tail item over to the slow loop below
+      sup = sup2;
+#pragma unroll
+      for (int k = 0; k < NS; k++) d[k] = d2[k];
       nch = nch2;
       return false;
     }
-    set = set2; chunk = chunk2; nch = nch2; d = d2; base_cur = base2;
+    sup = sup2; chunk = chunk2; nch = nch2;
+#pragma unroll
+    for (int k = 0; k < NS; k++) { d[k] = d2[k]; base_cur[k] = base2[k]; tr_cur[k] = tr2[k]; }
     return more;
   };
   {
-    uint4 A[JC], B[JC];
-    load_chunk<JC>(base_cur, 0, A);
+    ItemBuf<NS, JC> A, B;
+    load_item<NS, JC, SEAL, NO_TRAILER>(base_cur, tr_cur, 0, A);
     while (step(A, B) && step(B, A)) {
     }
   }
-  // Tail sets (last sets of the batch) through the slow path.
+  // Tail items (last of the batch) through the slow path.
   if (go_slow) {
-    for (; set < nsets; set += W) {
-      d = desc_now(set);
-      nch = wave_nch(d.J);
-      slow_set<FREEZE, SEAL>(L, p, set, d, nch * JC);
+    for (; sup < nsup; sup += W) {
+#pragma unroll
+      for (int k = 0; k < NS; k++) d[k] = desc_now(sup * NS + k);
+      nch = item_nch(d);
+      slow_item(sup, d, nch);
     }
   }
 }
 
-#define UFC_INSTANTIATE(JC)                                                          \
-  template __global__ void frame_crc_kernel<JC, 0>(const KernelParams);                 \
-  template __global__ void frame_crc_kernel<JC, kModeSeal>(const KernelParams);         \
-  template __global__ void frame_crc_kernel<JC, kModeVarlen>(const KernelParams);       \
-  template __global__ void frame_crc_kernel<JC, kModeVarlen | kModeSeal>(const KernelParams); \
-  template __global__ void frame_crc_kernel<JC, kModeFreeze>(const KernelParams);       \
-  template __global__ void frame_crc_kernel<JC, kModeFreeze | kModeSeal>(const KernelParams);
+#define UFC_INST_MODES(NS, JC)                                                                          \
+  template __global__ void frame_crc_kernel<NS, JC, 0>(const KernelParams);                             \
+  template __global__ void frame_crc_kernel<NS, JC, kModeSeal>(const KernelParams);                     \
+  template __global__ void frame_crc_kernel<NS, JC, kModeFreeze>(const KernelParams);                   \
+  template __global__ void frame_crc_kernel<NS, JC, kModeFreeze | kModeSeal>(const KernelParams);       \
+  template __global__ void frame_crc_kernel<NS, JC, kModeVarlen>(const KernelParams);                   \
+  template __global__ void frame_crc_kernel<NS, JC, kModeVarlen | kModeSeal>(const KernelParams);
 
-UFC_INSTANTIATE(1)
-UFC_INSTANTIATE(2)
-UFC_INSTANTIATE(3)
-UFC_INSTANTIATE(4)
-UFC_INSTANTIATE(5)
-UFC_INSTANTIATE(6)
+#define UFC_CONFIGS(X) X(1, 1) X(1, 2) X(1, 3) X(1, 6) X(2, 1) X(2, 2) X(2, 3) X(4, 1)
 
-const void* kernel_symbol(int jc, int mode) {
-#define UFC_PICK(JC)                                                                                      \
-  case JC:                                                                                                \
-    switch (mode) {                                                                                       \
-      case 0: return (const void*)frame_crc_kernel<JC, 0>;                                               \
-      case kModeSeal: return (const void*)frame_crc_kernel<JC, kModeSeal>;                               \
-      case kModeVarlen: return (const void*)frame_crc_kernel<JC, kModeVarlen>;                           \
-      case kModeVarlen | kModeSeal: return (const void*)frame_crc_kernel<JC, kModeVarlen | kModeSeal>;   \
-      case kModeFreeze: return (const void*)frame_crc_kernel<JC, kModeFreeze>;                           \
-      case kModeFreeze | kModeSeal: return (const void*)frame_crc_kernel<JC, kModeFreeze | kModeSeal>;   \
-      default: return nullptr;                                                                            \
-    }
-  switch (jc) {
-    UFC_PICK(1)
-    UFC_PICK(2)
-    UFC_PICK(3)
-    UFC_PICK(4)
-    UFC_PICK(5)
-    UFC_PICK(6)
-    default:
-      return nullptr;
+UFC_CONFIGS(UFC_INST_MODES)
+
+#ifdef UFC_TUNING
+template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute>(const KernelParams);
+template __global__ void frame_crc_kernel<1, 6, kModeAblateLoads>(const KernelParams);
+template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute | 32>(const KernelParams);
+template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64>(const KernelParams);
+template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64 | 128>(const KernelParams);
+template __global__ void frame_crc_kernel<1, 6, 32>(const KernelParams);
+template __global__ void frame_crc_kernel<1, 6, 64>(const KernelParams);
+#endif
+
+const void* kernel_symbol(int ns, int jc, int mode) {
+#define UFC_PICK(NS, JC)                                                                                   \
+  if (ns == NS && jc == JC) {                                                                              \
+    switch (mode) {                                                                                        \
+      case 0: return (const void*)frame_crc_kernel<NS, JC, 0>;                                            \
+      case kModeSeal: return (const void*)frame_crc_kernel<NS, JC, kModeSeal>;                            \
+      case kModeFreeze: return (const void*)frame_crc_kernel<NS, JC, kModeFreeze>;                        \
+      case kModeFreeze | kModeSeal: return (const void*)frame_crc_kernel<NS, JC, kModeFreeze | kModeSeal>;\
+      case kModeVarlen: return (const void*)frame_crc_kernel<NS, JC, kModeVarlen>;                        \
+      case kModeVarlen | kModeSeal: return (const void*)frame_crc_kernel<NS, JC, kModeVarlen | kModeSeal>;\
+      default: break;                                                                                      \
+    }                                                                                                      \
   }
+  UFC_CONFIGS(UFC_PICK)
 #undef UFC_PICK
+#ifdef UFC_TUNING
+  if (ns == 1 && jc == 6 && mode == kModeAblateCompute) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute>;
+  if (ns == 1 && jc == 6 && mode == kModeAblateLoads) return (const void*)frame_crc_kernel<1, 6, kModeAblateLoads>;
+  if (ns == 1 && jc == 6 && mode == (kModeAblateCompute | 32)) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute | 32>;
+  if (ns == 1 && jc == 6 && mode == (kModeAblateCompute | 32 | 64)) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64>;
+  if (ns == 1 && jc == 6 && mode == (kModeAblateCompute | 32 | 64 | 128)) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64 | 128>;
+  if (ns == 1 && jc == 6 && mode == 32) return (const void*)frame_crc_kernel<1, 6, 32>;
+  if (ns == 1 && jc == 6 && mode == 64) return (const void*)frame_crc_kernel<1, 6, 64>;
+#endif
+  return nullptr;
+}
+
+bool config_available(int ns, int jc) {
+#define UFC_HAVE(NS, JC) if (ns == NS && jc == JC) return true;
+  UFC_CONFIGS(UFC_HAVE)
+#undef UFC_HAVE
+  return false;
 }
 
 }  // namespace ufc_dev

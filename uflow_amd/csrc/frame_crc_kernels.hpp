@@ -7,6 +7,9 @@ namespace ufc_dev {
 constexpr int kModeVarlen = 1;  // frames from a CSR offsets array
 constexpr int kModeSeal = 2;    // write the BE32 trailer instead of validating it
 constexpr int kModeFreeze = 4;  // fixed-length frames whose block count is not a multiple of JC
+// Ablation modes, instantiated only in tuning builds (-DUFC_TUNING): results are meaningless.
+constexpr int kModeAblateCompute = 8;   // loads only (data XOR-folded, no CRC)
+constexpr int kModeAblateLoads = 16;    // CRC compute on register data, no loads after the first item
 
 constexpr int kBlockThreads = 1024;          // one workgroup per CU, 16 waves
 constexpr int kLdsBytes = 131072 + 32768;    // chain tables + nibble tables
@@ -26,7 +29,9 @@ struct KernelParams {
   uint32_t G;                 // A^-4(~0)
 };
 
-// Kernel entry for (JC blocks per chunk, mode); nullptr if not instantiated.
-const void* kernel_symbol(int jc, int mode);
+// Kernel entry for (NS frame sets per wave-iteration, JC blocks per chunk, mode); nullptr if
+// that configuration is not instantiated.
+const void* kernel_symbol(int ns, int jc, int mode);
+bool config_available(int ns, int jc);
 
 }  // namespace ufc_dev

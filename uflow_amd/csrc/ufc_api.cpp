@@ -4,6 +4,7 @@
 // frame_crc.hip.  Batched calls never fall back to the CPU.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -53,12 +54,28 @@ int hip_fail(ufc_ctx* ctx, hipError_t e) {
   return UFC_ERR_HIP;
 }
 
-int launch(ufc_ctx* ctx, int jc, int mode, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  const void* fn = ufc_dev::kernel_symbol(jc, mode);
+struct Config {
+  int ns, jc;
+};
+
+// Optional tuning override, e.g. UFC_FIXED_CFG="2,3" (frame sets per wave-iteration, blocks per chunk).
+bool env_config(const char* name, Config* c) {
+  const char* v = std::getenv(name);
+  if (!v) return false;
+  int ns = 0, jc = 0;
+  if (std::sscanf(v, "%d,%d", &ns, &jc) != 2 || !ufc_dev::config_available(ns, jc)) return false;
+  c->ns = ns;
+  c->jc = jc;
+  return true;
+}
+
+int launch(ufc_ctx* ctx, Config cfg, int mode, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  const void* fn = ufc_dev::kernel_symbol(cfg.ns, cfg.jc, mode);
   if (!fn) return UFC_ERR_INVALID_ARG;
   const uint64_t nsets = (kp.nframes + 3) / 4;
+  const uint64_t nsup = (nsets + cfg.ns - 1) / cfg.ns;
   const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
-  uint64_t blocks = (nsets + waves_per_block - 1) / waves_per_block;
+  uint64_t blocks = (nsup + waves_per_block - 1) / waves_per_block;
   if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
   if (blocks < 1) blocks = 1;
   kp.chain_tab = ctx->d_chain;
@@ -71,17 +88,29 @@ int launch(ufc_ctx* ctx, int jc, int mode, ufc_dev::KernelParams& kp, hipStream_
   return UFC_OK;
 }
 
-// Blocks-per-chunk and mode bits for a fixed frame length.
-void fixed_geometry(uint64_t frame_len, int* jc, int* freeze) {
+// Kernel configuration and mode bits for a fixed frame length: J = 256-byte blocks per frame.
+Config fixed_config(uint64_t frame_len, int* freeze) {
   const uint64_t n = frame_len >= 4 ? frame_len - 4 : frame_len;
   const uint64_t J = (n + 4 + 255) / 256;
-  if (J <= 6) {
-    *jc = (int)J;
-    *freeze = 0;
-  } else {  // long frames: chunks of 4 blocks
-    *jc = 4;
-    *freeze = (J % 4) ? ufc_dev::kModeFreeze : 0;
+  Config c;
+  if (!env_config("UFC_FIXED_CFG", &c)) {
+    switch (J) {
+      case 1: c = {4, 1}; break;
+      case 2: c = {2, 2}; break;
+      case 3: c = {2, 3}; break;
+      case 4: c = {2, 2}; break;
+      case 5: c = {4, 1}; break;
+      default: c = {2, 3}; break;
+    }
   }
+  *freeze = (J % (uint64_t)c.jc) ? ufc_dev::kModeFreeze : 0;
+  return c;
+}
+
+Config varlen_config() {
+  Config c = {1, 3};
+  env_config("UFC_VARLEN_CFG", &c);
+  return c;
 }
 
 constexpr uint64_t kMaxFrameLen = (uint64_t)1 << 30;  // per-frame limit of the 32-bit offsets math
@@ -164,11 +193,18 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
     ufc_ctx_destroy(ctx);
     return UFC_ERR_HIP;
   }
-  for (int jc : {1, 2, 3, 4, 5, 6})
+  for (int ns : {1, 2, 3, 4})
+    for (int jc = 1; jc <= 8; jc++)
     for (int mode : {0, ufc_dev::kModeSeal, ufc_dev::kModeVarlen, ufc_dev::kModeVarlen | ufc_dev::kModeSeal,
                      ufc_dev::kModeFreeze, ufc_dev::kModeFreeze | ufc_dev::kModeSeal}) {
-      e = hipFuncSetAttribute(ufc_dev::kernel_symbol(jc, mode), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              ufc_dev::kLdsBytes);
+      const void* fn = ufc_dev::kernel_symbol(ns, jc, mode);
+      if (!fn) continue;
+#ifdef UFC_TUNING
+      for (int ab : {ufc_dev::kModeAblateCompute, ufc_dev::kModeAblateLoads, 8 | 32, 8 | 32 | 64, 8 | 32 | 64 | 128, 32, 64})
+        if (const void* fa = ufc_dev::kernel_symbol(ns, jc, ab))
+          (void)hipFuncSetAttribute(fa, hipFuncAttributeMaxDynamicSharedMemorySize, ufc_dev::kLdsBytes);
+#endif
+      e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, ufc_dev::kLdsBytes);
       if (e != hipSuccess) {
         ufc_ctx_destroy(ctx);
         return UFC_ERR_HIP;
@@ -202,8 +238,11 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
   if (n == 0) return UFC_OK;
   if (!d_frames || stride < frame_len || frame_len > kMaxFrameLen || (!d_crc_out && !d_valid_out))
     return UFC_ERR_INVALID_ARG;
-  int jc, freeze;
-  fixed_geometry(frame_len, &jc, &freeze);
+  int freeze;
+  const Config cfg = fixed_config(frame_len, &freeze);
+#ifdef UFC_TUNING
+  if (const char* ab = std::getenv("UFC_ABLATE")) freeze |= std::atoi(ab);
+#endif
   ufc_dev::KernelParams kp{};
   kp.bytes = d_frames;
   kp.stride = stride;
@@ -212,7 +251,7 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
-  return launch(ctx, jc, freeze, kp, (hipStream_t)stream);
+  return launch(ctx, cfg, freeze, kp, (hipStream_t)stream);
 }
 
 int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
@@ -227,7 +266,7 @@ int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
-  return launch(ctx, 6, ufc_dev::kModeVarlen, kp, (hipStream_t)stream);
+  return launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, (hipStream_t)stream);
 }
 
 int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
@@ -235,8 +274,8 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   if (!ctx) return UFC_ERR_INVALID_ARG;
   if (n == 0) return UFC_OK;
   if (!d_frames || stride < frame_len || frame_len < 4 || frame_len > kMaxFrameLen) return UFC_ERR_INVALID_ARG;
-  int jc, freeze;
-  fixed_geometry(frame_len, &jc, &freeze);
+  int freeze;
+  const Config cfg = fixed_config(frame_len, &freeze);
   ufc_dev::KernelParams kp{};
   kp.bytes = d_frames;
   kp.wbytes = d_frames;
@@ -245,7 +284,7 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
-  return launch(ctx, jc, freeze | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
+  return launch(ctx, cfg, freeze | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
 
 int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
@@ -260,7 +299,7 @@ int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offs
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
-  return launch(ctx, 6, ufc_dev::kModeVarlen | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
+  return launch(ctx, varlen_config(), ufc_dev::kModeVarlen | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
 
 int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
@@ -345,7 +384,7 @@ int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_
     kp.nframes = nf;
     kp.crc_out = dcrc;
     kp.valid_out = dval;
-    int rc = launch(ctx, 6, ufc_dev::kModeVarlen, kp, s);
+    int rc = launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, s);
     if (rc != UFC_OK) return rc;
     if (h_crc_out && (e = hipMemcpyAsync(h_crc_out + a, dcrc, nf * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
       return hip_fail(ctx, e);
