@@ -59,6 +59,23 @@ def test_fixed_large_batch_with_flips(engine):
     assert valid.sum() == 20000 - 20
 
 
+@pytest.mark.parametrize("frame_len,n", [(64, 3), (64, 4 * 4096 - 1), (1500, 4 * 4096 * 2 + 3), (1500, 70001),
+                                         (250, 123457), (1531, 9999)])
+def test_fixed_exact_buffer_partition(engine, frame_len, n):
+    """Buffer ends exactly at the last frame's end; sizes straddle the per-wave set partition."""
+    rng = np.random.default_rng(frame_len * 7 + n)
+    stride = frame_len
+    buf = _rand_bytes(rng, n * stride)
+    oracle.seal_fixed(buf, stride, frame_len, n)
+    for i in range(0, n, 37):
+        buf[i * stride + int(rng.integers(0, frame_len))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    ref_crc, ref_valid = oracle.validate_fixed(buf, stride, frame_len, n)
+    crc, valid = engine.crc_fixed(torch.from_numpy(buf).to(DEV), frame_len, stride=stride, n=n)
+    torch.cuda.synchronize()
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc)
+    assert np.array_equal(valid.cpu().numpy(), ref_valid)
+
+
 def test_fixed_kat(engine):
     frame = bytearray(b"123456789" + b"\0\0\0\0")
     oracle.frame_seal(frame)

@@ -4,7 +4,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 OUT=$R/gpurun_out/${1:-ablate}
 mkdir -p $OUT
-export UFC_LIB=$R/uflow_amd/libuflowcrc_tuning.so UFC_FIXED_CFG=${CFG:-1,6}
+export UFC_LIB=$R/uflow_amd/libuflowcrc_tuning.so UFC_FIXED_JC=${CFG:-6}
 for rep in 1 2; do
 for ab in ${ABS:-0 8 16}; do
   UFC_ABLATE=$ab timeout -k 10 200 python bench.py --no-cpu-baseline --steps 40 > $OUT/ab_$ab.json 2>$OUT/ab_$ab.err

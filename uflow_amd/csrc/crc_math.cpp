@@ -129,7 +129,7 @@ void build_nibble_image(uint32_t out[8192]) {
     const int s = ((c & 31) << 1) | (c >> 5);
     for (int k = 0; k < 8; k++)
       for (int e = 0; e < 16; e++)
-        out[(k * 16 + e) * 64 + c] = advance((uint32_t)e << (4 * k), (uint64_t)4 * (64 - s));
+        out[(k * 16 + e) * 64 + c] = advance((uint32_t)e << (4 * k), (uint64_t)4 * (63 - s));
   }
 }
 

@@ -36,7 +36,7 @@ uint32_t host_extend(uint32_t initial_crc, const uint8_t* data, size_t len);
 
 // Device table images (layouts documented in frame_crc.hip):
 //   chain[k*256 + e] = A^256(e << 8k)                       k = 0..3, e = 0..255   (1024 words)
-//   nib[(k*16 + e)*64 + c] = A^(4(64 - s))(e << 4k),  s = ((c & 31) << 1) | (c >> 5)  (8192 words)
+//   nib[(k*16 + e)*64 + c] = A^(4(63 - s))(e << 4k),  s = ((c & 31) << 1) | (c >> 5)  (8192 words)
 void build_chain_table(uint32_t out[1024]);
 void build_nibble_image(uint32_t out[8192]);
 

@@ -5,22 +5,28 @@
 // (src/frame/serial/mod.rs:463-470, src/frame/serial/build.rs:151-159).
 //
 // Algorithm (all linear over GF(2), register domain; see crc_math.hpp):
-//   * A frame's n CRC bytes are right-aligned into a virtual stream of J*256 bytes:
-//       [ zeros | G (4 bytes) | frame[0..n) ],  J = ceil((n+4)/256),  pad = 256*J - n  (4..259).
-//     G = A^-4(~0) makes the linear CRC of the stream equal the reference's register after
-//     init ~0, so crc = ~lin(stream).
+//   * A frame of len bytes has n = len-4 CRC'd bytes followed by the 4-byte trailer (n = len and
+//     4 virtual zero bytes when len < 4).  With E = n + 4 the frame is right-aligned into a virtual
+//     stream of J*256 bytes:
+//         [ zeros | G (4 bytes) | frame[0..n) | T (4 bytes) ],  J = ceil((E+4)/256),  pad = 256J - E,
+//     so frame offset o sits at virtual byte o + pad (pad in 4..259).  G = A^-4(~0) folds the
+//     reference's init (~0) into a plain linear CRC.  T is the trailer: it is the LAST virtual word,
+//     arrives with the coalesced block loads, is kept for the validity check and is replaced by zero
+//     in the CRC; the zero word's A^4 is undone by the slot constants below.
 //   * Virtual word w (4 bytes) belongs to slot s = w mod 64.  Slot s runs a Horner chain over the
 //     J blocks with the constant A^256:  V_s <- A^256(V_s) ^ word.  A^256 is applied with four
 //     byte tables held in LDS, replicated 32x so that lane l always reads bank l mod 32
 //     (conflict-free ds_read_b32 whatever the data).
-//   * lin = XOR_s A^(4(64-s))(V_s): each slot's final value is multiplied by its own constant via
-//     per-slot nibble tables in LDS (8 lookups), then XOR-reduced inside the frame's 16 lanes
-//     with DPP.
-// Wave layout: 4 frames per wave, 16 lanes per frame; lane col of a frame loads the 16 bytes
-// at 16*col of each 256-byte block with one global_load_dwordx4 (non-temporal), so a
-// wave-instruction reads four contiguous 256-byte runs.  Lane col holds slots 4*col+b (b=0..3)
-// in four independent chains.  Frames whose block count differs inside a wave (varlen) run the
-// wave's maximum and freeze their chains after their own last block.
+//   * lin = XOR_s A^(4(63-s))(V_s)  (= A^-4 of the stream's linear CRC, i.e. the register after
+//     frame[0..n) with init ~0); crc = ~lin.  Each slot's value is multiplied by its constant via
+//     per-slot nibble tables in LDS (8 lookups), then XOR-reduced in the frame's 16 lanes by DPP.
+// Wave layout: 4 frames per set, 16 lanes per frame; lane col of a frame loads the 16 bytes at
+// 16*col of each 256-byte block with one non-temporal global_load_dwordx4, so a wave-instruction
+// reads four contiguous 256-byte runs.  Lane col holds slots 4*col+b (b=0..3) in four independent
+// chains.  A wave walks contiguous runs of kSetsPerRun sets (64 frames): results accumulate in
+// registers (lane i <-> frame i of the run) and leave as one coalesced store per run.  Frames
+// whose block count differs inside a set (varlen) run the set's maximum and freeze their chains
+// after their own last block.
 //
 // LDS (one 1024-thread workgroup per CU, 160 KiB), laid out so that every table address is ONE
 // v_perm_b32 (byte select) of the value being looked up:
@@ -53,9 +59,7 @@ __device__ __forceinline__ G* as_global(T* p) {
   return (G*)(p);
 }
 
-__device__ __forceinline__ uint32_t lds_ld(const char* lds, uint32_t byteoff) {
-  return *(const uint32_t*)(lds + byteoff);
-}
+constexpr int kSetsPerRun = 16;  // 16 sets x 4 frames = 64 frames = one result per lane
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
@@ -83,8 +87,8 @@ __device__ __forceinline__ uint32_t chain_step(const char* lds, uint32_t v, uint
   return xor3(xor3(r0, r1, r2), r3, x);
 }
 
-// Multiply v by the constant of the slot whose column byte-offset is byte `i` of K2:
-// nibble k of v indexes row (k*16 + e); address bytes [K2.byte_i, nibble, 0, 0] + k*4096.
+// Multiply v by the constant of the slot whose column byte-offset is byte I of K2:
+// nibble k of v indexes row (k*16 + e); address bytes [K2.byte_I, nibble, 0, 0] + k*4096.
 template <int I>
 __device__ __forceinline__ uint32_t nib_mul(const char* lds, uint32_t v, uint32_t K2) {
   const uint32_t lo = v & 0x0F0F0F0Fu;          // nibbles 0,2,4,6 as bytes
@@ -95,7 +99,7 @@ __device__ __forceinline__ uint32_t nib_mul(const char* lds, uint32_t v, uint32_
     const uint32_t sel = 0x0C0C0000u | ((uint32_t)(4 + (k >> 1)) << 8) | (uint32_t)I;
     r[k] = *(const uint32_t*)(lds + perm((k & 1) ? hi : lo, K2, sel) + k * 4096);
   }
-  return xor3(xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6]), r[7], 0u);
+  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], 0u));
 }
 
 // XOR over the 16 lanes of a DPP row; every lane of the row receives the total.
@@ -111,7 +115,7 @@ __device__ __forceinline__ uint32_t row_xor16(uint32_t v) {
 // Bytes at frame offsets [-4, 0) are G's bytes, below -4 zeros, from 0 on the loaded data v.
 __device__ __forceinline__ uint32_t fix_word(uint32_t v, int o, uint32_t G) {
   const uint64_t pv = (uint64_t)G << 32;
-  const int sh = 8 * (o + 8);                       // in [8, 56] when o in (-8, 0)
+  const int sh = 8 * (o + 8);  // in [8, 56] when o in (-8, 0)
   const uint32_t pre = (uint32_t)(pv >> (sh & 63));
   const uint32_t dm = (o > -4) ? (0xFFFFFFFFu << ((8 * (-o)) & 31)) : 0u;
   const uint32_t mixed = (v & dm) | (pre & ~dm);
@@ -124,7 +128,7 @@ struct FrameDesc {
   uint32_t len;    // frame length (bytes)
   uint32_t n;      // CRC'd bytes: len - 4, or len when len < 4
   int J;           // 256-byte blocks of the virtual stream
-  int pad;         // 256*J - n  (4..259)
+  int pad;         // 256*J - (n + 4)
 };
 
 __device__ __forceinline__ FrameDesc make_desc(uint64_t start, uint64_t len64) {
@@ -132,13 +136,15 @@ __device__ __forceinline__ FrameDesc make_desc(uint64_t start, uint64_t len64) {
   d.start = start;
   d.len = (uint32_t)len64;
   d.n = d.len >= 4u ? d.len - 4u : d.len;
-  d.J = (int)((d.n + 4u + 255u) >> 8);
-  d.pad = d.J * 256 - (int)d.n;
+  const uint32_t E = d.n + 4u;
+  d.J = (int)((E + 4u + 255u) >> 8);
+  d.pad = d.J * 256 - (int)E;
   return d;
 }
 
 struct Lane {
   const char* lds;
+  int lane;       // 0..63
   int col;        // lane within the frame's 16-lane group
   int grp;        // frame group 0..3 inside the wave
   bool odd;       // grp & 1
@@ -149,12 +155,19 @@ struct Lane {
 
 struct Chains {
   uint32_t v0, v1, v2, v3;
+  uint32_t tr;    // the frame's trailer word (lane col 15 only)
 };
 
 // One 256-byte block of the virtual stream: front fix (block 0, and the single word of block 1
-// that straddles the G/data boundary when pad > 256), then the A^256 Horner step.
+// that straddles the G/data boundary when pad > 256), trailer capture on the last block, then the
+// A^256 Horner step.
 template <bool FREEZE>
 __device__ __forceinline__ void process_block(const Lane& L, const FrameDesc& d, int blk, uint4 x, Chains& c) {
+  {  // the last block's lane-15 last word is the trailer T: keep it, CRC it as zero
+    const bool t = (L.col == 15) && (blk == d.J - 1);
+    c.tr = t ? x.w : c.tr;
+    x.w = t ? 0u : x.w;
+  }
   if (blk == 0) {
     const int o = 16 * L.col - d.pad;
     c.v0 = fix_word(x.x, o, L.G);
@@ -179,160 +192,195 @@ __device__ __forceinline__ void process_block(const Lane& L, const FrameDesc& d,
   }
 }
 
-// Slot constants, 16-lane XOR, outputs of one frame set.
+// Per-run output accumulators: lane i holds the results of frame i of the run.
+struct RunAcc {
+  uint32_t crc;
+  uint32_t valid;
+};
+
+// Slot constants + 16-lane XOR -> the frame's CRC (in every lane of its group); validity from the
+// trailer (lane 15 of the group); results written into the run accumulators at lanes 4t + g.
+// Seal mode writes the trailer here.
 template <bool SEAL>
-__device__ __forceinline__ void finish_set(const Lane& L, const KernelParams& p, uint64_t set, const FrameDesc& d,
-                                           const Chains& c, uint32_t trailer_le) {
+__device__ __forceinline__ void finish_set(const Lane& L, const KernelParams& p, const FrameDesc& d, const Chains& c,
+                                           uint64_t set, int t, RunAcc& acc) {
   const uint32_t X0 = L.odd ? c.v2 : c.v0, X1 = L.odd ? c.v3 : c.v1;
   const uint32_t X2 = L.odd ? c.v0 : c.v2, X3 = L.odd ? c.v1 : c.v3;
-  uint32_t acc = xor3(nib_mul<0>(L.lds, X0, L.K2), nib_mul<1>(L.lds, X1, L.K2), nib_mul<2>(L.lds, X2, L.K2)) ^
+  uint32_t lin = xor3(nib_mul<0>(L.lds, X0, L.K2), nib_mul<1>(L.lds, X1, L.K2), nib_mul<2>(L.lds, X2, L.K2)) ^
                  nib_mul<3>(L.lds, X3, L.K2);
-  acc = row_xor16(acc);
-  const uint32_t crc = ~acc;
-  const uint64_t f = set * 4 + (uint64_t)L.grp;
-  if (L.col == 0 && f < p.nframes) {
-    if (SEAL) {
-      if (d.len >= 4u) {
-        g_u8w* t = as_global<g_u8w>(p.wbytes + d.start + d.n);
-        t[0] = (uint8_t)(crc >> 24);
-        t[1] = (uint8_t)(crc >> 16);
-        t[2] = (uint8_t)(crc >> 8);
-        t[3] = (uint8_t)crc;
+  lin = row_xor16(lin);
+  const uint32_t crc = ~lin;
+  if (SEAL) {
+    const uint64_t f = set * 4 + (uint64_t)L.grp;
+    if (L.col == 15 && f < p.nframes && d.len >= 4u) {
+      uint8_t* a = p.wbytes + d.start + d.n;
+      if (((uintptr_t)a & 3u) == 0) {
+        *as_global<g_u32w>((uint32_t*)a) = __builtin_bswap32(crc);
+      } else {
+        g_u8w* w = as_global<g_u8w>(a);
+        w[0] = (uint8_t)(crc >> 24);
+        w[1] = (uint8_t)(crc >> 16);
+        w[2] = (uint8_t)(crc >> 8);
+        w[3] = (uint8_t)crc;
       }
-      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crc;
-    } else {
-      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crc;
-      if (p.valid_out) {
-        uint8_t ok = 0;
-        if (d.len >= 5u) ok = (__builtin_bswap32(trailer_le) == crc) ? 1 : 0;
-        *as_global<g_u8w>(p.valid_out + f) = ok;
-      }
+    }
+  }
+  const uint32_t ok = (d.len >= 5u && __builtin_bswap32(c.tr) == crc) ? 1u : 0u;
+  // gather: frame g of this set -> lane 4t + g of the run accumulators
+  const int dst = L.lane - 4 * t;  // in [0, 4) for the 4 lanes receiving this set's results
+#pragma unroll
+  for (int g = 0; g < 4; g++) {
+    const uint32_t cg = __builtin_amdgcn_readlane(crc, 16 * g);
+    acc.crc = (dst == g) ? cg : acc.crc;
+    if (!SEAL) {
+      const uint32_t vg = __builtin_amdgcn_readlane(ok, 16 * g + 15);
+      acc.valid = (dst == g) ? vg : acc.valid;
     }
   }
 }
 
-// Slow path for a whole frame set (edge/tail sets: frames whose fast loads could leave the
-// buffer).  Byte loads restricted to [0, n) of the frame, one block at a time, not unrolled, so
-// that it adds no register pressure to the fast path.
-template <bool FREEZE, bool SEAL>
-__device__ __forceinline__ void slow_set(const Lane& L, const KernelParams& p, uint64_t set, const FrameDesc& d,
-                                         int nblocks) {
-  Chains c{0u, 0u, 0u, 0u};
+// Store a run's results (frames run_first .. run_first + 63, clipped to nframes): one coalesced
+// dword store of CRC words and one coalesced byte store of valid flags per wave.
+template <bool SEAL>
+__device__ __forceinline__ void store_run(const Lane& L, const KernelParams& p, uint64_t run_first, const RunAcc& acc) {
+  const uint64_t f = run_first + (uint64_t)L.lane;
+  if (f < p.nframes) {
+    if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = acc.crc;
+    if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)acc.valid;
+  }
+}
+
+// Slow path for one set (edge/tail sets: frames whose fast loads could leave the buffer).  Byte
+// loads restricted to [0, len) of the frame, one block at a time, not unrolled, so that it adds no
+// register pressure to the fast path.
+template <bool SEAL>
+__device__ __forceinline__ void slow_set(const Lane& L, const KernelParams& p, const FrameDesc& d, int nblocks,
+                                         uint64_t set, int t, RunAcc& acc) {
+  Chains c{0u, 0u, 0u, 0u, 0u};
 #pragma unroll 1
   for (int blk = 0; blk < nblocks; blk++) {
     const int bl = min(blk, d.J - 1);
     uint32_t w[4];
 #pragma unroll
     for (int b = 0; b < 4; b++) {
-      const int o = 256 * bl + 16 * L.col + 4 * b - d.pad;
-      uint32_t acc = 0;
+      const int o = 256 * bl + 16 * L.col + 4 * b - d.pad;  // frame offset of the word
+      uint32_t a = 0;
 #pragma unroll 1
       for (int k = 0; k < 4; k++) {
         const int ob = o + k;
-        if (ob >= 0 && ob < (int)d.n) acc |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
+        if (ob >= 0 && ob < (int)d.len) a |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
       }
-      w[b] = acc;
+      w[b] = a;
     }
     process_block<true>(L, d, blk, make_uint4(w[0], w[1], w[2], w[3]), c);
   }
-  uint32_t tr = 0;
-  if (!SEAL && d.len >= 5u) {
-    g_u8* t = as_global<g_u8>(p.bytes + d.start + d.n);
-    tr = (uint32_t)t[0] | ((uint32_t)t[1] << 8) | ((uint32_t)t[2] << 16) | ((uint32_t)t[3] << 24);
-  }
-  finish_set<SEAL>(L, p, set, d, c, tr);
+  finish_set<SEAL>(L, p, d, c, set, t, acc);
 }
 
-// Fast-path item buffer: JC blocks of each of the NS frame sets of a wave-iteration, plus the
-// frames' trailer words.  The trailer word is loaded together with the data so that no load
-// is issued after the next item's prefetch (in-order vmcnt would force a wait on it).
-template <int NS, int JC>
+// Stage the tables into LDS: one global round trip per thread (blockDim.x == 1024).
+__device__ __forceinline__ void stage_tables(const KernelParams& p, char* lds) {
+  const int t = threadIdx.x;
+  const uint32_t cv = *as_global<g_u32>(p.chain_tab + t);
+  const u32x4 n0 = *as_global<g_u32x4>(p.nib_img + 8 * t);
+  const u32x4 n1 = *as_global<g_u32x4>(p.nib_img + 8 * t + 4);
+  const uint32_t k = (uint32_t)t >> 8, e = (uint32_t)t & 255u;
+  const uint32_t cbase = kChainBase + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+  const u32x4 cr = {cv, cv, cv, cv};
+#pragma unroll
+  for (int i = 0; i < 8; i++) *(u32x4*)(lds + cbase + 16 * i) = cr;
+  *(u32x4*)(lds + 32 * t) = n0;
+  *(u32x4*)(lds + 32 * t + 16) = n1;
+  __syncthreads();
+}
+
+__device__ __forceinline__ void init_lane(Lane& L, char* lds, uint32_t G) {
+  L.lds = lds;
+  L.lane = threadIdx.x & 63;
+  L.col = L.lane & 15;
+  L.grp = L.lane >> 4;
+  L.odd = (L.grp & 1) != 0;
+  L.G = G;
+  const uint32_t c4 = (uint32_t)(L.lane & 31) * 4u;
+  L.K = c4 | ((c4 + 128u) << 8) | (1u << 24);
+  uint32_t k2 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int sl = 4 * L.col + ((i + (L.odd ? 2 : 0)) & 3);
+    k2 |= (uint32_t)(((sl >> 1) + 32 * (sl & 1)) * 4) << (8 * i);
+  }
+  L.K2 = k2;
+}
+
+// lin of the frame held by this 16-lane group (every lane of the group receives it).
+__device__ __forceinline__ uint32_t group_lin(const Lane& L, const Chains& c) {
+  const uint32_t X0 = L.odd ? c.v2 : c.v0, X1 = L.odd ? c.v3 : c.v1;
+  const uint32_t X2 = L.odd ? c.v0 : c.v2, X3 = L.odd ? c.v1 : c.v3;
+  const uint32_t lin = xor3(nib_mul<0>(L.lds, X0, L.K2), nib_mul<1>(L.lds, X1, L.K2), nib_mul<2>(L.lds, X2, L.K2)) ^
+                       nib_mul<3>(L.lds, X3, L.K2);
+  return row_xor16(lin);
+}
+
+// Fast-path item buffer: JC blocks of the set's four frames (one 16-byte piece per lane each).
+template <int JC>
 struct ItemBuf {
-  uint4 x[NS][JC];
-  uint32_t tr[NS];  // 4 trailer bytes (little-endian load); validate mode only
+  uint4 x[JC];
 };
 
-template <int NS, int JC, bool SEAL, bool NO_TRAILER = false>
-__device__ __forceinline__ void load_item(const uint8_t* const (&lane_base)[NS], const uint8_t* const (&trailer)[NS],
-                                          int chunk, ItemBuf<NS, JC>& b) {
+template <int JC>
+__device__ __forceinline__ void load_item(const uint8_t* lane_base, int part, ItemBuf<JC>& b) {
+  const uint8_t* q = lane_base + (int64_t)part * (JC * 256);
 #pragma unroll
-  for (int k = 0; k < NS; k++) {
-    const uint8_t* q = lane_base[k] + (int64_t)chunk * (JC * 256);
-#pragma unroll
-    for (int j = 0; j < JC; j++) {
-      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
-      b.x[k][j] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-    if (!SEAL && !NO_TRAILER) b.tr[k] = *as_global<g_u32>(trailer[k]);
-    if (NO_TRAILER) b.tr[k] = 0;
+  for (int j = 0; j < JC; j++) {
+    const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
+    b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
   }
 }
 
-// Blocks j of all NS sets are processed back to back (j outer, k inner): 4*NS independent
-// chains per lane hide the LDS latency of each Horner step.
-template <int NS, int JC, bool FREEZE, bool CHUNK0>
-__device__ __forceinline__ void compute_item(const Lane& L, const FrameDesc (&d)[NS], int chunk,
-                                             const ItemBuf<NS, JC>& b, Chains (&c)[NS]) {
+template <int JC, bool FREEZE, bool PART0>
+__device__ __forceinline__ void compute_item(const Lane& L, const FrameDesc& d, int part, const ItemBuf<JC>& b,
+                                             Chains& c) {
 #pragma unroll
-  for (int j = 0; j < JC; j++)
-#pragma unroll
-    for (int k = 0; k < NS; k++) process_block<FREEZE>(L, d[k], CHUNK0 ? j : chunk * JC + j, b.x[k][j], c[k]);
+  for (int j = 0; j < JC; j++) process_block<FREEZE>(L, d, PART0 ? j : part * JC + j, b.x[j], c);
 }
 
-template <int NS, int JC, int MODE>
+template <int JC, int MODE>
 __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
   constexpr bool VARLEN = (MODE & kModeVarlen) != 0;
   constexpr bool SEAL = (MODE & kModeSeal) != 0;
-  constexpr bool FREEZE = VARLEN || (MODE & kModeFreeze) != 0;  // blocks past J may occur in a chunk
+  constexpr bool FREEZE = VARLEN || (MODE & kModeFreeze) != 0;  // blocks past J may occur in a part
+  // Fixed-length frames without freeze: the host picks JC == J, so every set is one part.
+  constexpr bool SINGLE = !VARLEN && (MODE & kModeFreeze) == 0;
   constexpr bool NO_COMPUTE = (MODE & kModeAblateCompute) != 0;  // tuning builds only
   constexpr bool NO_LOADS = (MODE & kModeAblateLoads) != 0;      // tuning builds only
-  constexpr bool NO_TRAILER = (MODE & 32) != 0;                  // tuning builds only
-  constexpr bool NO_STORES = (MODE & 64) != 0;                   // tuning builds only
-  constexpr bool NO_STAGING = (MODE & 128) != 0;                 // tuning builds only
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  // ---- stage the tables into LDS: one global round trip per thread ----
-  if (!NO_STAGING) {
-    const int t = threadIdx.x;  // blockDim.x == 1024 (set by the launcher)
-    const uint32_t cv = *as_global<g_u32>(p.chain_tab + t);
-    const u32x4 n0 = *as_global<g_u32x4>(p.nib_img + 8 * t);
-    const u32x4 n1 = *as_global<g_u32x4>(p.nib_img + 8 * t + 4);
-    const uint32_t k = (uint32_t)t >> 8, e = (uint32_t)t & 255u;
-    const uint32_t cbase = kChainBase + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
-    const u32x4 cr = {cv, cv, cv, cv};
-#pragma unroll
-    for (int i = 0; i < 8; i++) *(u32x4*)(lds + cbase + 16 * i) = cr;
-    *(u32x4*)(lds + 32 * t) = n0;
-    *(u32x4*)(lds + 32 * t + 16) = n1;
-  }
-  __syncthreads();
+  // Static LDS (all 160 KiB): its base is the constant 0, so a perm result IS the LDS address (a
+  // dynamic-LDS base would cost one v_add per table lookup).
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  stage_tables(p, lds);
 
   Lane L;
-  L.lds = lds;
-  const int lane = threadIdx.x & 63;
-  L.col = lane & 15;
-  L.grp = lane >> 4;
-  L.odd = (L.grp & 1) != 0;
-  {
-    const uint32_t c4 = (uint32_t)(lane & 31) * 4u;
-    L.K = c4 | ((c4 + 128u) << 8) | (1u << 24);
-    uint32_t k2 = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int s = 4 * L.col + ((i + (L.odd ? 2 : 0)) & 3);
-      k2 |= (uint32_t)(((s >> 1) + 32 * (s & 1)) * 4) << (8 * i);
-    }
-    L.K2 = k2;
-  }
-  L.G = p.G;
-  const uint64_t nsets = (p.nframes + 3) >> 2;        // 4 frames per set (one per 16-lane group)
-  const uint64_t nsup = (nsets + NS - 1) / NS;        // NS sets per wave-iteration
+  init_lane(L, lds, p.G);
+  const uint64_t nsets = (p.nframes + 3) >> 2;  // 4 frames per set (one per 16-lane group)
   const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  // Wave-uniform item counter, made provably uniform (SGPR) so that loop control compiles to
-  // scalar branches and no load sits behind an exec mask.
+  // Wave-uniform counters, provably uniform (SGPR) so that loop control compiles to scalar
+  // branches and no load sits behind an exec mask.
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint64_t sup = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
-  if (sup >= nsup) return;
-  // End of the readable batch bytes (fast loads must stay below it).
+  const uint64_t w0 = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  // Set sequence of this wave: runs r = w0, w0 + W, ...; run r covers sets [r*R, r*R + R).
+  constexpr int R = kSetsPerRun;
+  uint64_t run = w0;
+  int t = 0;  // set index inside the run
+  if (run * R >= nsets) return;
+  auto set_of = [&](uint64_t r, int tt) -> uint64_t { return r * R + (uint64_t)tt; };
+  // next set in this wave's sequence: advance t, or jump to the next run
+  auto next_pos = [&](uint64_t r, int tt, uint64_t& r2, int& t2) {
+    if (tt + 1 < R && set_of(r, tt + 1) < nsets) {
+      r2 = r;
+      t2 = tt + 1;
+    } else {
+      r2 = r + W;
+      t2 = 0;
+    }
+  };
   const uint64_t buf_end =
       VARLEN ? *as_global<g_u64>(p.offsets + p.nframes) : (p.nframes - 1) * p.stride + p.frame_len;
 
@@ -355,225 +403,425 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
     m = max(m, __builtin_amdgcn_readlane(v, 48));
     return m;
   };
-  auto item_nch = [&](const FrameDesc (&dd)[NS]) -> int {
-    int m = 0;
-#pragma unroll
-    for (int k = 0; k < NS; k++) m = max(m, dd[k].J);
-    return (wave_max(m) + JC - 1) / JC;
-  };
-  // Fast loads read [start - pad, start - pad + 256*JC*nch) of every frame: stay in the buffer.
-  auto item_slow = [&](const FrameDesc (&dd)[NS], int nch) -> bool {
-    int bad = 0;
-#pragma unroll
-    for (int k = 0; k < NS; k++)
-      bad |= (dd[k].start < (uint64_t)dd[k].pad ||
-              dd[k].start - dd[k].pad + (uint64_t)(256 * JC) * nch > buf_end) ? 1 : 0;
+  auto set_parts = [&](const FrameDesc& dd) -> int { return (wave_max(dd.J) + JC - 1) / JC; };
+  // Fast loads read [start - pad, start - pad + 256*JC*parts) of every frame: stay in the buffer.
+  auto set_slow = [&](const FrameDesc& dd, int parts) -> bool {
+    const int bad =
+        (dd.start < (uint64_t)dd.pad || dd.start - dd.pad + (uint64_t)(256 * JC) * parts > buf_end) ? 1 : 0;
     return wave_max(bad) != 0;
   };
-  auto trailer_ptr = [&](const FrameDesc& dd) -> const uint8_t* {
-    return p.bytes + dd.start + (dd.len >= 4u ? dd.n : 0u);  // frames without trailer: harmless address
-  };
-  auto slow_item = [&](uint64_t s, const FrameDesc (&dd)[NS], int nch) {
-#pragma unroll 1
-    for (int k = 0; k < NS; k++)
-      if (s * NS + k < nsets) slow_set<FREEZE, SEAL>(L, p, s * NS + k, dd[k], nch * JC);
+
+  RunAcc acc{0u, 0u};
+  // After set (r, tt): store the run's results when the run ends.
+  auto after_set = [&](uint64_t r, int tt) {
+    uint64_t r2;
+    int t2;
+    next_pos(r, tt, r2, t2);
+    if (r2 != r) store_run<SEAL>(L, p, set_of(r, 0) * 4, acc);
   };
 
-  FrameDesc d[NS];
-#pragma unroll
-  for (int k = 0; k < NS; k++) d[k] = desc_now(sup * NS + k);
-  int nch = item_nch(d);
-  // Edge items (first sets of the batch) through the slow path.
-  while (item_slow(d, nch)) {
-    slow_item(sup, d, nch);
-    sup += W;
-    if (sup >= nsup) return;
-#pragma unroll
-    for (int k = 0; k < NS; k++) d[k] = desc_now(sup * NS + k);
-    nch = item_nch(d);
+  FrameDesc d = desc_now(set_of(run, t));
+  int parts = set_parts(d);
+  // Edge sets (first sets of the batch) through the slow path.
+  while (set_slow(d, parts)) {
+    slow_set<SEAL>(L, p, d, parts * JC, set_of(run, t), t, acc);
+    after_set(run, t);
+    next_pos(run, t, run, t);
+    if (set_of(run, t) >= nsets) return;
+    d = desc_now(set_of(run, t));
+    parts = set_parts(d);
   }
 
-  // Varlen: the offsets of the NEXT item are loaded one item ahead.
-  uint64_t pre_a[NS], pre_b[NS];
-  auto prefetch_offsets = [&](uint64_t s2) {
+  // ---- fast path: items (set, part) in a 3-deep software pipeline ----
+  // Cursor of one item.  valid/slow are wave-uniform.
+  struct Cursor {
+    uint64_t run;
+    int t, part, parts;
+    bool valid, slow;
+    FrameDesc d;
+  };
+  // Varlen: offsets of the set after the leading cursor's set, loaded one set ahead.
+  uint64_t pre_a = 0, pre_b = 0;
+  auto prefetch_offsets = [&](uint64_t r2, int t2) {
     if (VARLEN) {
-#pragma unroll
-      for (int k = 0; k < NS; k++) {
-        const uint64_t f = frame_index((s2 < nsup ? s2 : sup) * NS + k);
-        pre_a[k] = *as_global<g_u64>(p.offsets + f);
-        pre_b[k] = *as_global<g_u64>(p.offsets + f + 1);
-      }
+      const uint64_t s2 = set_of(r2, t2);
+      const uint64_t f = frame_index(s2 < nsets ? s2 : 0);
+      pre_a = *as_global<g_u64>(p.offsets + f);
+      pre_b = *as_global<g_u64>(p.offsets + f + 1);
     }
   };
-  auto desc_next = [&](uint64_t s2, FrameDesc (&dd)[NS]) {
-#pragma unroll
-    for (int k = 0; k < NS; k++)
-      dd[k] = VARLEN ? make_desc(pre_a[k], pre_b[k] - pre_a[k]) : make_desc(frame_index(s2 * NS + k) * p.stride, p.frame_len);
-  };
-  prefetch_offsets(sup + W);
-
-  // Main loop, double-buffered over items (super-set, chunk): the next item's loads are in
-  // flight while the current one is computed.  Buffers alternate explicitly (a register copy
-  // would make hipcc wait for every outstanding load at the loop head).
-  Chains c[NS];
-  int chunk = 0;
-  const uint8_t* base_cur[NS];
-  const uint8_t* tr_cur[NS];
-#pragma unroll
-  for (int k = 0; k < NS; k++) {
-    base_cur[k] = p.bytes + d[k].start - d[k].pad + 16 * L.col;
-    tr_cur[k] = trailer_ptr(d[k]);
-  }
-  bool go_slow = false;  // the next item needs the slow path (tail of the batch)
-  auto step = [&](ItemBuf<NS, JC>& cur, ItemBuf<NS, JC>& nxt) -> bool {
-    uint64_t sup2 = sup;
-    int chunk2 = chunk + 1, nch2 = nch;
-    FrameDesc d2[NS];
-    const uint8_t* base2[NS];
-    const uint8_t* tr2[NS];
-#pragma unroll
-    for (int k = 0; k < NS; k++) { d2[k] = d[k]; base2[k] = base_cur[k]; tr2[k] = tr_cur[k]; }
-    const bool newitem = (chunk2 == nch);
-    bool more = true;
-    if (newitem) {
-      sup2 = sup + W;
-      chunk2 = 0;
-      more = sup2 < nsup;
-      if (more) {
-        desc_next(sup2, d2);
-        nch2 = item_nch(d2);
-        prefetch_offsets(sup2 + W);
-        if (item_slow(d2, nch2)) {
-          go_slow = true;
-          more = false;
-        }
-#pragma unroll
-        for (int k = 0; k < NS; k++) {
-          base2[k] = p.bytes + d2[k].start - d2[k].pad + 16 * L.col;
-          tr2[k] = trailer_ptr(d2[k]);
-        }
-      }
+  // Advance the leading cursor to the next item of the wave's sequence.
+  auto advance = [&](Cursor& c) {
+    if (!c.valid || c.slow) {
+      c.valid = false;
+      return;
     }
-    // Unconditional prefetch (the last one re-reads the current item): a load behind a branch
-    // makes the waitcnt pass assume it was skipped and wait for the whole prefetch.
+    if (!SINGLE && c.part + 1 < c.parts) {
+      c.part++;
+      return;
+    }
+    uint64_t r2;
+    int t2;
+    next_pos(c.run, c.t, r2, t2);
+    c.run = r2;
+    c.t = t2;
+    c.part = 0;
+    if (set_of(r2, t2) >= nsets) {
+      c.valid = false;
+      return;
+    }
+    c.d = VARLEN ? make_desc(pre_a, pre_b - pre_a) : make_desc(frame_index(set_of(r2, t2)) * p.stride, p.frame_len);
     {
-      const uint8_t* lb[NS];
-      const uint8_t* lt[NS];
+      uint64_t r3;
+      int t3;
+      next_pos(r2, t2, r3, t3);
+      prefetch_offsets(r3, t3);
+    }
+    c.parts = set_parts(c.d);
+    c.slow = set_slow(c.d, c.parts);
+  };
+  auto lane_base = [&](const Cursor& c) -> const uint8_t* { return p.bytes + c.d.start - c.d.pad + 16 * L.col; };
+
+  Cursor C0{run, t, 0, parts, true, false, d};
+  {
+    uint64_t r2;
+    int t2;
+    next_pos(run, t, r2, t2);
+    prefetch_offsets(r2, t2);
+  }
+  Cursor C1 = C0;
+  advance(C1);
+  Cursor C2 = C1;
+  advance(C2);
+  // A fast load of a cursor that is not a fast item re-reads C0's first part (harmless, in bounds).
+  auto load_cursor = [&](const Cursor& c, ItemBuf<JC>& b) {
+    const bool ok = c.valid && !c.slow;
+    load_item<JC>(ok ? lane_base(c) : lane_base(C0), ok ? c.part : 0, b);
+  };
+
+  Chains c{0u, 0u, 0u, 0u, 0u};
+  bool go_slow = false;  // the sequence continues with a slow (tail) set
+  uint64_t slow_run = 0;
+  int slow_t = 0;
+  // One pipeline step: issue the loads of C2 into `nxt2` (the buffer of the item computed last
+  // step), compute C0 from `cur`, shift the cursors.  Loads are unconditional: a load behind a
+  // branch makes the waitcnt pass assume it was skipped and wait for the whole prefetch.
+  auto step = [&](ItemBuf<JC>& cur, ItemBuf<JC>& nxt2) -> bool {
+    if (NO_LOADS) {
 #pragma unroll
-      for (int k = 0; k < NS; k++) { lb[k] = more ? base2[k] : base_cur[k]; lt[k] = more ? tr2[k] : tr_cur[k]; }
-      if (NO_LOADS) {
-#pragma unroll
-        for (int k = 0; k < NS; k++)
-#pragma unroll
-          for (int j = 0; j < JC; j++) nxt.x[k][j] = make_uint4(cur.x[k][j].y, cur.x[k][j].z, cur.x[k][j].w, cur.x[k][j].x ^ chunk2);
-      } else {
-        load_item<NS, JC, SEAL, NO_TRAILER>(lb, lt, more ? chunk2 : chunk, nxt);
-      }
+      for (int j = 0; j < JC; j++) nxt2.x[j] = make_uint4(cur.x[j].y, cur.x[j].z, cur.x[j].w, cur.x[j].x ^ C2.part);
     }
     if (NO_COMPUTE) {
+      if (!NO_LOADS) load_cursor(C2, nxt2);
 #pragma unroll
-      for (int k = 0; k < NS; k++)
+      for (int j = 0; j < JC; j++) c.v0 ^= cur.x[j].x ^ cur.x[j].y ^ cur.x[j].z ^ cur.x[j].w;
+      c.tr = c.v0;
+    } else {
+      // The prefetch of C2 is spread over the compute of C0, one block load per block of compute,
+      // pinned by sched_barrier: a wave that issued all its loads up front would stall at VMEM issue
+      // behind the other waves' bursts instead of computing.
+      const bool ok = C2.valid && !C2.slow;
+      const uint8_t* q = (ok ? lane_base(C2) : lane_base(C0)) + (int64_t)(ok ? C2.part : 0) * (JC * 256);
+      const bool p0 = SINGLE || C0.part == 0;
+      if (!p0) __builtin_assume(C0.part >= 1);
 #pragma unroll
-        for (int j = 0; j < JC; j++) c[k].v0 ^= cur.x[k][j].x ^ cur.x[k][j].y ^ cur.x[k][j].z ^ cur.x[k][j].w;
-    } else if (chunk == 0)
-      compute_item<NS, JC, FREEZE, true>(L, d, 0, cur, c);
-    else {
-      __builtin_assume(chunk >= 1);
-      compute_item<NS, JC, FREEZE, false>(L, d, chunk, cur, c);
-    }
-    if (newitem) {
-#pragma unroll
-      for (int k = 0; k < NS; k++) {
-        if (NO_STORES) {
-          if (c[k].v0 == 0x12345678u && c[k].v1 == cur.tr[k]) *as_global<g_u32w>(p.crc_out) = 1u;  // keep live
-        } else {
-          finish_set<SEAL>(L, p, sup * NS + k, d[k], c[k], cur.tr[k]);
+      for (int j = 0; j < JC; j++) {
+        if (!NO_LOADS) {
+          const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
+          nxt2.x[j] = make_uint4(v.x, v.y, v.z, v.w);
         }
+        __builtin_amdgcn_sched_barrier(0);
+        if (p0)
+          process_block<FREEZE>(L, C0.d, j, cur.x[j], c);
+        else
+          process_block<FREEZE>(L, C0.d, C0.part * JC + j, cur.x[j], c);
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
-    if (go_slow) {  // hand the tail item over to the slow loop below
-      sup = sup2;
-#pragma unroll
-      for (int k = 0; k < NS; k++) d[k] = d2[k];
-      nch = nch2;
+    if (SINGLE || C0.part + 1 == C0.parts) {
+      finish_set<SEAL>(L, p, C0.d, c, set_of(C0.run, C0.t), C0.t, acc);
+      after_set(C0.run, C0.t);
+    }
+    if (!C1.valid) return false;
+    if (C1.slow) {
+      go_slow = true;
+      slow_run = C1.run;
+      slow_t = C1.t;
       return false;
     }
-    sup = sup2; chunk = chunk2; nch = nch2;
-#pragma unroll
-    for (int k = 0; k < NS; k++) { d[k] = d2[k]; base_cur[k] = base2[k]; tr_cur[k] = tr2[k]; }
-    return more;
+    C0 = C1;
+    C1 = C2;
+    advance(C2);
+    return true;
   };
   {
-    ItemBuf<NS, JC> A, B;
-    load_item<NS, JC, SEAL, NO_TRAILER>(base_cur, tr_cur, 0, A);
-    while (step(A, B) && step(B, A)) {
+    ItemBuf<JC> X, Y, Z;
+    load_cursor(C0, X);
+    load_cursor(C1, Y);
+    while (step(X, Z) && step(Y, X) && step(Z, Y)) {
     }
   }
-  // Tail items (last of the batch) through the slow path.
+  // Tail sets (last of the batch) through the slow path.
   if (go_slow) {
-    for (; sup < nsup; sup += W) {
-#pragma unroll
-      for (int k = 0; k < NS; k++) d[k] = desc_now(sup * NS + k);
-      nch = item_nch(d);
-      slow_item(sup, d, nch);
+    run = slow_run;
+    t = slow_t;
+    while (set_of(run, t) < nsets) {
+      d = desc_now(set_of(run, t));
+      parts = set_parts(d);
+      slow_set<SEAL>(L, p, d, parts * JC, set_of(run, t), t, acc);
+      after_set(run, t);
+      next_pos(run, t, run, t);
     }
   }
 }
 
-#define UFC_INST_MODES(NS, JC)                                                                          \
-  template __global__ void frame_crc_kernel<NS, JC, 0>(const KernelParams);                             \
-  template __global__ void frame_crc_kernel<NS, JC, kModeSeal>(const KernelParams);                     \
-  template __global__ void frame_crc_kernel<NS, JC, kModeFreeze>(const KernelParams);                   \
-  template __global__ void frame_crc_kernel<NS, JC, kModeFreeze | kModeSeal>(const KernelParams);       \
-  template __global__ void frame_crc_kernel<NS, JC, kModeVarlen>(const KernelParams);                   \
-  template __global__ void frame_crc_kernel<NS, JC, kModeVarlen | kModeSeal>(const KernelParams);
 
-#define UFC_CONFIGS(X) X(1, 1) X(1, 2) X(1, 3) X(1, 6) X(2, 1) X(2, 2) X(2, 3) X(4, 1)
+// ---------------------------------------------------------------------------------------------
+// Lean kernel for fixed-length frames (frame_len >= 4, J = ceil((frame_len+4)/256) <= 6 blocks,
+// known at compile time): the batched gate of BASELINE.json configs 2 and 4.  Each wave owns a
+// balanced contiguous range of sets; loop-invariant geometry (front-fix masks, lane offsets) is
+// hoisted, set addresses are scalar, results gather with one select per set.
+// ---------------------------------------------------------------------------------------------
+template <int J, bool SEAL>
+__global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  stage_tables(p, lds);
+  Lane L;
+  init_lane(L, lds, p.G);
+
+  const uint64_t stride = p.stride;
+  const uint32_t len = (uint32_t)p.frame_len;  // >= 4 (host checks)
+  const uint32_t n = len - 4u;
+  const int pad = J * 256 - (int)len;          // E = len
+  const uint64_t nsets = (p.nframes + 3) >> 2;
+  const uint64_t NW = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
+  const uint64_t s_begin = nsets * w / NW, s_end = nsets * (w + 1) / NW;
+  if (s_begin >= s_end) return;
+  // Sets before s_fast have a frame whose pad region precedes the buffer: slow path.
+  const uint64_t s_fast = ((uint64_t)pad + 4 * stride - 1) / (4 * stride);
+
+  // Loop invariants of this lane.
+  const int64_t lane_off = (int64_t)L.grp * (int64_t)stride + 16 * L.col - pad;
+  uint32_t dm[4], pre[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const int o = 16 * L.col + 4 * b - pad;
+    const uint32_t fz = fix_word(0u, o, L.G);           // G/zero part
+    const uint32_t f1 = fix_word(0xFFFFFFFFu, o, L.G);  // data mask | G part
+    dm[b] = f1 & ~fz;  // data bytes
+    pre[b] = fz;
+  }
+  uint32_t dm1, pre1;
+  {
+    const int o = 256 + 16 * L.col - pad;
+    const uint32_t fz = fix_word(0u, o, L.G), f1 = fix_word(0xFFFFFFFFu, o, L.G);
+    dm1 = f1 & ~fz;
+    pre1 = fz;
+  }
+  const uint32_t tmask = (L.col == 15) ? 0u : 0xFFFFFFFFu;  // zero the trailer word in the CRC
+
+  // frame results of the current run of 16 sets: lane (g, col=t) <- crc of frame 4t+g;
+  // lane 15 of group g collects valid bit t of frame 4t+g.
+  uint32_t acc_crc = 0, acc_vbits = 0;
+  auto store_run = [&](uint64_t run_set0, int nset_in_run) {
+    uint32_t vb = 0;
+#pragma unroll
+    for (int g = 0; g < 4; g++) {
+      const uint32_t m = __builtin_amdgcn_readlane(acc_vbits, 16 * g + 15);
+      vb = (L.grp == g) ? m : vb;
+    }
+    const uint64_t f = (run_set0 + (uint64_t)L.col) * 4 + (uint64_t)L.grp;
+    if (L.col < nset_in_run && f < p.nframes) {
+      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = acc_crc;
+      if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)((vb >> L.col) & 1u);
+    }
+  };
+  // Finish set s (t = its index in the current run).
+  auto finish = [&](uint64_t s, int t, const Chains& c) {
+    const uint32_t crc = ~group_lin(L, c);
+    acc_crc = (L.col == t) ? crc : acc_crc;
+    if (SEAL) {
+      const uint64_t f = s * 4 + (uint64_t)L.grp;
+      if (L.col == 15 && f < p.nframes) {
+        uint8_t* a = p.wbytes + f * stride + n;
+        if (((uintptr_t)a & 3u) == 0) {
+          *as_global<g_u32w>((uint32_t*)a) = __builtin_bswap32(crc);
+        } else {
+          g_u8w* wp = as_global<g_u8w>(a);
+          wp[0] = (uint8_t)(crc >> 24);
+          wp[1] = (uint8_t)(crc >> 16);
+          wp[2] = (uint8_t)(crc >> 8);
+          wp[3] = (uint8_t)crc;
+        }
+      }
+    } else {
+      const uint32_t ok = (len >= 5u && __builtin_bswap32(c.tr) == crc) ? 1u : 0u;
+      acc_vbits |= ok << t;  // meaningful in lane 15 of each group
+    }
+  };
+  // Frame-set processing from a loaded item (J blocks).
+  auto compute = [&](const ItemBuf<J>& b, Chains& c) {
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      uint4 x = b.x[j];
+      if (j == J - 1) {
+        c.tr = x.w;
+        x.w &= tmask;
+      }
+      if (j == 0) {
+        c.v0 = (x.x & dm[0]) | pre[0];
+        c.v1 = (x.y & dm[1]) | pre[1];
+        c.v2 = (x.z & dm[2]) | pre[2];
+        c.v3 = (x.w & dm[3]) | pre[3];
+      } else {
+        if (j == 1) x.x = (x.x & dm1) | pre1;
+        c.v0 = chain_step(L.lds, c.v0, L.K, x.x);
+        c.v1 = chain_step(L.lds, c.v1, L.K, x.y);
+        c.v2 = chain_step(L.lds, c.v2, L.K, x.z);
+        c.v3 = chain_step(L.lds, c.v3, L.K, x.w);
+      }
+    }
+  };
+  auto lane_ptr = [&](uint64_t s) -> const uint8_t* {
+    return p.bytes + s * 4 * stride + lane_off;  // s*4*stride is wave-uniform
+  };
+
+  uint64_t s = s_begin;
+  uint64_t run0 = s_begin;
+  // Edge sets: slow path (they are the first sets of the batch).
+  for (; s < s_end && s < s_fast; s++) {
+    const int t = (int)(s - run0);
+    FrameDesc d = make_desc(min(s * 4 + (uint64_t)L.grp, p.nframes - 1) * stride, len);
+    Chains c{0u, 0u, 0u, 0u, 0u};
+#pragma unroll 1
+    for (int blk = 0; blk < J; blk++) {
+      uint32_t wv[4];
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        const int o = 256 * blk + 16 * L.col + 4 * b - d.pad;
+        uint32_t a = 0;
+#pragma unroll 1
+        for (int k = 0; k < 4; k++) {
+          const int ob = o + k;
+          if (ob >= 0 && ob < (int)d.len) a |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
+        }
+        wv[b] = a;
+      }
+      process_block<false>(L, d, blk, make_uint4(wv[0], wv[1], wv[2], wv[3]), c);
+    }
+    finish(s, t, c);
+    if (t == kSetsPerRun - 1 || s + 1 == s_end) {
+      store_run(run0, t + 1);
+      run0 = s + 1;
+      acc_vbits = 0;
+    }
+  }
+  if (s >= s_end) return;
+  // The last set may hold frames past nframes: those lanes re-read frame nframes-1 (loads never
+  // leave the buffer) and their results are not stored.  Only the final set pays the clamp.
+  auto safe_ptr = [&](uint64_t ss) -> const uint8_t* {
+    const uint64_t room = p.nframes - 1 - 4 * ss;  // >= 0 for every set < nsets
+    const int64_t over = (int64_t)L.grp - (int64_t)min(room, (uint64_t)3);
+    return lane_ptr(ss) - (over > 0 ? over * (int64_t)stride : 0);
+  };
+
+  // Main loop: double-buffered over sets.
+  Chains c{0u, 0u, 0u, 0u, 0u};
+  auto load = [&](uint64_t ss, ItemBuf<J>& b) {
+    const uint8_t* q = safe_ptr(ss < s_end ? ss : s);
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
+      b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+  auto step = [&](ItemBuf<J>& cur, ItemBuf<J>& nxt) -> bool {
+    load(s + 1, nxt);
+    compute(cur, c);
+    const int t = (int)(s - run0);
+    finish(s, t, c);
+    s++;
+    if (t == kSetsPerRun - 1 || s == s_end) {
+      store_run(run0, t + 1);
+      run0 = s;
+      acc_vbits = 0;
+    }
+    return s < s_end;
+  };
+  {
+    ItemBuf<J> A, B;
+    load(s, A);
+    while (step(A, B) && step(B, A)) {
+    }
+  }
+}
+
+template __global__ void frame_crc_fixed_kernel<1, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<2, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<3, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<4, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<5, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<1, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<2, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<3, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<4, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<5, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, true>(const KernelParams);
+
+const void* fixed_kernel_symbol(int J, bool seal) {
+  switch (J) {
+    case 1: return seal ? (const void*)frame_crc_fixed_kernel<1, true> : (const void*)frame_crc_fixed_kernel<1, false>;
+    case 2: return seal ? (const void*)frame_crc_fixed_kernel<2, true> : (const void*)frame_crc_fixed_kernel<2, false>;
+    case 3: return seal ? (const void*)frame_crc_fixed_kernel<3, true> : (const void*)frame_crc_fixed_kernel<3, false>;
+    case 4: return seal ? (const void*)frame_crc_fixed_kernel<4, true> : (const void*)frame_crc_fixed_kernel<4, false>;
+    case 5: return seal ? (const void*)frame_crc_fixed_kernel<5, true> : (const void*)frame_crc_fixed_kernel<5, false>;
+    case 6: return seal ? (const void*)frame_crc_fixed_kernel<6, true> : (const void*)frame_crc_fixed_kernel<6, false>;
+    default: return nullptr;
+  }
+}
+
+#define UFC_INST_MODES(JC)                                                                          \
+  template __global__ void frame_crc_kernel<JC, 0>(const KernelParams);                             \
+  template __global__ void frame_crc_kernel<JC, kModeSeal>(const KernelParams);                     \
+  template __global__ void frame_crc_kernel<JC, kModeFreeze>(const KernelParams);                   \
+  template __global__ void frame_crc_kernel<JC, kModeFreeze | kModeSeal>(const KernelParams);       \
+  template __global__ void frame_crc_kernel<JC, kModeVarlen>(const KernelParams);                   \
+  template __global__ void frame_crc_kernel<JC, kModeVarlen | kModeSeal>(const KernelParams);
+
+#define UFC_CONFIGS(X) X(1) X(2) X(3) X(4) X(5) X(6)
 
 UFC_CONFIGS(UFC_INST_MODES)
 
 #ifdef UFC_TUNING
-template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute>(const KernelParams);
-template __global__ void frame_crc_kernel<1, 6, kModeAblateLoads>(const KernelParams);
-template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute | 32>(const KernelParams);
-template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64>(const KernelParams);
-template __global__ void frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64 | 128>(const KernelParams);
-template __global__ void frame_crc_kernel<1, 6, 32>(const KernelParams);
-template __global__ void frame_crc_kernel<1, 6, 64>(const KernelParams);
+template __global__ void frame_crc_kernel<6, kModeAblateCompute>(const KernelParams);
+template __global__ void frame_crc_kernel<6, kModeAblateLoads>(const KernelParams);
 #endif
 
-const void* kernel_symbol(int ns, int jc, int mode) {
-#define UFC_PICK(NS, JC)                                                                                   \
-  if (ns == NS && jc == JC) {                                                                              \
-    switch (mode) {                                                                                        \
-      case 0: return (const void*)frame_crc_kernel<NS, JC, 0>;                                            \
-      case kModeSeal: return (const void*)frame_crc_kernel<NS, JC, kModeSeal>;                            \
-      case kModeFreeze: return (const void*)frame_crc_kernel<NS, JC, kModeFreeze>;                        \
-      case kModeFreeze | kModeSeal: return (const void*)frame_crc_kernel<NS, JC, kModeFreeze | kModeSeal>;\
-      case kModeVarlen: return (const void*)frame_crc_kernel<NS, JC, kModeVarlen>;                        \
-      case kModeVarlen | kModeSeal: return (const void*)frame_crc_kernel<NS, JC, kModeVarlen | kModeSeal>;\
-      default: break;                                                                                      \
-    }                                                                                                      \
+const void* kernel_symbol(int jc, int mode) {
+#define UFC_PICK(JC)                                                                                   \
+  if (jc == JC) {                                                                                      \
+    switch (mode) {                                                                                    \
+      case 0: return (const void*)frame_crc_kernel<JC, 0>;                                            \
+      case kModeSeal: return (const void*)frame_crc_kernel<JC, kModeSeal>;                            \
+      case kModeFreeze: return (const void*)frame_crc_kernel<JC, kModeFreeze>;                        \
+      case kModeFreeze | kModeSeal: return (const void*)frame_crc_kernel<JC, kModeFreeze | kModeSeal>; \
+      case kModeVarlen: return (const void*)frame_crc_kernel<JC, kModeVarlen>;                        \
+      case kModeVarlen | kModeSeal: return (const void*)frame_crc_kernel<JC, kModeVarlen | kModeSeal>; \
+      default: break;                                                                                  \
+    }                                                                                                  \
   }
   UFC_CONFIGS(UFC_PICK)
 #undef UFC_PICK
 #ifdef UFC_TUNING
-  if (ns == 1 && jc == 6 && mode == kModeAblateCompute) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute>;
-  if (ns == 1 && jc == 6 && mode == kModeAblateLoads) return (const void*)frame_crc_kernel<1, 6, kModeAblateLoads>;
-  if (ns == 1 && jc == 6 && mode == (kModeAblateCompute | 32)) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute | 32>;
-  if (ns == 1 && jc == 6 && mode == (kModeAblateCompute | 32 | 64)) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64>;
-  if (ns == 1 && jc == 6 && mode == (kModeAblateCompute | 32 | 64 | 128)) return (const void*)frame_crc_kernel<1, 6, kModeAblateCompute | 32 | 64 | 128>;
-  if (ns == 1 && jc == 6 && mode == 32) return (const void*)frame_crc_kernel<1, 6, 32>;
-  if (ns == 1 && jc == 6 && mode == 64) return (const void*)frame_crc_kernel<1, 6, 64>;
+  if (jc == 6 && mode == kModeAblateCompute) return (const void*)frame_crc_kernel<6, kModeAblateCompute>;
+  if (jc == 6 && mode == kModeAblateLoads) return (const void*)frame_crc_kernel<6, kModeAblateLoads>;
 #endif
   return nullptr;
 }
 
-bool config_available(int ns, int jc) {
-#define UFC_HAVE(NS, JC) if (ns == NS && jc == JC) return true;
-  UFC_CONFIGS(UFC_HAVE)
-#undef UFC_HAVE
-  return false;
-}
+bool config_available(int jc) { return jc >= 1 && jc <= 6; }
 
 }  // namespace ufc_dev

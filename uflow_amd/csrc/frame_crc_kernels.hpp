@@ -13,7 +13,6 @@ constexpr int kModeAblateLoads = 16;    // CRC compute on register data, no load
 
 constexpr int kBlockThreads = 1024;          // one workgroup per CU, 16 waves
 constexpr int kLdsBytes = 131072 + 32768;    // chain tables + nibble tables
-constexpr int kFramesPerBlockIter = 64;      // 16 waves x 4 frames
 
 struct KernelParams {
   const uint8_t* bytes;       // batch base (fixed) or CSR byte buffer (varlen)
@@ -25,13 +24,15 @@ struct KernelParams {
   uint32_t* crc_out;          // nullable
   uint8_t* valid_out;         // nullable (validate mode)
   const uint32_t* chain_tab;  // device: 1024 words (A^256 byte tables)
-  const uint32_t* nib_img;    // device: 8192 words (per-slot nibble tables, LDS image)
+  const uint32_t* nib_img;    // device: 8192 words (per-slot nibble tables, LDS image order)
   uint32_t G;                 // A^-4(~0)
 };
 
-// Kernel entry for (NS frame sets per wave-iteration, JC blocks per chunk, mode); nullptr if
-// that configuration is not instantiated.
-const void* kernel_symbol(int ns, int jc, int mode);
-bool config_available(int ns, int jc);
+// Kernel entry for (JC 256-byte blocks per pipelined part, mode); nullptr if not instantiated.
+const void* kernel_symbol(int jc, int mode);
+bool config_available(int jc);
+// Lean fixed-length kernel (frame_len >= 4, J = ceil((frame_len + 4) / 256) in 1..6); one
+// workgroup per CU, each wave a balanced contiguous range of 4-frame sets.
+const void* fixed_kernel_symbol(int J, bool seal);
 
 }  // namespace ufc_dev

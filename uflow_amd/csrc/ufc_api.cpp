@@ -55,35 +55,64 @@ int hip_fail(ufc_ctx* ctx, hipError_t e) {
 }
 
 struct Config {
-  int ns, jc;
+  int jc;  // 256-byte blocks per pipelined part
 };
 
-// Optional tuning override, e.g. UFC_FIXED_CFG="2,3" (frame sets per wave-iteration, blocks per chunk).
+// Optional tuning override, e.g. UFC_FIXED_JC=3.
 bool env_config(const char* name, Config* c) {
   const char* v = std::getenv(name);
   if (!v) return false;
-  int ns = 0, jc = 0;
-  if (std::sscanf(v, "%d,%d", &ns, &jc) != 2 || !ufc_dev::config_available(ns, jc)) return false;
-  c->ns = ns;
+  const int jc = std::atoi(v);
+  if (!ufc_dev::config_available(jc)) return false;
   c->jc = jc;
   return true;
 }
 
 int launch(ufc_ctx* ctx, Config cfg, int mode, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  const void* fn = ufc_dev::kernel_symbol(cfg.ns, cfg.jc, mode);
+  const void* fn = ufc_dev::kernel_symbol(cfg.jc, mode);
   if (!fn) return UFC_ERR_INVALID_ARG;
+  // A wave walks runs of 16 sets (64 frames); one 1024-thread workgroup per CU.
   const uint64_t nsets = (kp.nframes + 3) / 4;
-  const uint64_t nsup = (nsets + cfg.ns - 1) / cfg.ns;
+  const uint64_t nruns = (nsets + 15) / 16;
   const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
-  uint64_t blocks = (nsup + waves_per_block - 1) / waves_per_block;
+  uint64_t blocks = (nruns + waves_per_block - 1) / waves_per_block;
   if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
   if (blocks < 1) blocks = 1;
   kp.chain_tab = ctx->d_chain;
   kp.nib_img = ctx->d_nib;
   kp.G = ctx->G;
   void* args[] = {&kp};
-  hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args,
-                                 (size_t)ufc_dev::kLdsBytes, stream);
+  hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
+  if (e != hipSuccess) return hip_fail(ctx, e);
+  return UFC_OK;
+}
+
+// Lean fixed-length kernel: J = blocks per frame when 4 <= frame_len and J <= 6, else 0.  The
+// generic kernel stays reachable with UFC_FIXED_KERNEL=generic (A/B measurement) or UFC_FIXED_JC.
+int lean_fixed_blocks(uint64_t frame_len) {
+  if (frame_len < 4) return 0;
+  const uint64_t J = (frame_len + 4 + 255) / 256;
+  if (J > 6) return 0;
+  const char* k = std::getenv("UFC_FIXED_KERNEL");
+  if (k && std::strcmp(k, "generic") == 0) return 0;
+  if (std::getenv("UFC_FIXED_JC")) return 0;
+  return (int)J;
+}
+
+int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal);
+  if (!fn) return UFC_ERR_INVALID_ARG;
+  // Each wave takes a balanced contiguous range of sets; no more waves than sets.
+  const uint64_t nsets = (kp.nframes + 3) / 4;
+  const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
+  uint64_t blocks = (nsets + waves_per_block - 1) / waves_per_block;
+  if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
+  if (blocks < 1) blocks = 1;
+  kp.chain_tab = ctx->d_chain;
+  kp.nib_img = ctx->d_nib;
+  kp.G = ctx->G;
+  void* args[] = {&kp};
+  hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
   if (e != hipSuccess) return hip_fail(ctx, e);
   return UFC_OK;
 }
@@ -91,25 +120,17 @@ int launch(ufc_ctx* ctx, Config cfg, int mode, ufc_dev::KernelParams& kp, hipStr
 // Kernel configuration and mode bits for a fixed frame length: J = 256-byte blocks per frame.
 Config fixed_config(uint64_t frame_len, int* freeze) {
   const uint64_t n = frame_len >= 4 ? frame_len - 4 : frame_len;
-  const uint64_t J = (n + 4 + 255) / 256;
+  const uint64_t J = (n + 8 + 255) / 256;  // virtual stream: G + n bytes + trailer, 256-B blocks
   Config c;
-  if (!env_config("UFC_FIXED_CFG", &c)) {
-    switch (J) {
-      case 1: c = {4, 1}; break;
-      case 2: c = {2, 2}; break;
-      case 3: c = {2, 3}; break;
-      case 4: c = {2, 2}; break;
-      case 5: c = {4, 1}; break;
-      default: c = {2, 3}; break;
-    }
-  }
-  *freeze = (J % (uint64_t)c.jc) ? ufc_dev::kModeFreeze : 0;
+  if (!env_config("UFC_FIXED_JC", &c)) c.jc = J <= 6 ? (int)J : 6;
+  // Without freeze the kernel assumes one part per set (JC == J); anything else runs in freeze mode.
+  *freeze = ((uint64_t)c.jc == J) ? 0 : ufc_dev::kModeFreeze;
   return c;
 }
 
 Config varlen_config() {
-  Config c = {1, 3};
-  env_config("UFC_VARLEN_CFG", &c);
+  Config c = {3};
+  env_config("UFC_VARLEN_JC", &c);
   return c;
 }
 
@@ -193,23 +214,7 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
     ufc_ctx_destroy(ctx);
     return UFC_ERR_HIP;
   }
-  for (int ns : {1, 2, 3, 4})
-    for (int jc = 1; jc <= 8; jc++)
-    for (int mode : {0, ufc_dev::kModeSeal, ufc_dev::kModeVarlen, ufc_dev::kModeVarlen | ufc_dev::kModeSeal,
-                     ufc_dev::kModeFreeze, ufc_dev::kModeFreeze | ufc_dev::kModeSeal}) {
-      const void* fn = ufc_dev::kernel_symbol(ns, jc, mode);
-      if (!fn) continue;
-#ifdef UFC_TUNING
-      for (int ab : {ufc_dev::kModeAblateCompute, ufc_dev::kModeAblateLoads, 8 | 32, 8 | 32 | 64, 8 | 32 | 64 | 128, 32, 64})
-        if (const void* fa = ufc_dev::kernel_symbol(ns, jc, ab))
-          (void)hipFuncSetAttribute(fa, hipFuncAttributeMaxDynamicSharedMemorySize, ufc_dev::kLdsBytes);
-#endif
-      e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, ufc_dev::kLdsBytes);
-      if (e != hipSuccess) {
-        ufc_ctx_destroy(ctx);
-        return UFC_ERR_HIP;
-      }
-    }
+  // The kernels declare their 160 KiB of LDS statically: no dynamic-LDS attribute to set.
   *out = ctx;
   return UFC_OK;
 }
@@ -240,8 +245,12 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
     return UFC_ERR_INVALID_ARG;
   int freeze;
   const Config cfg = fixed_config(frame_len, &freeze);
+  int lean = lean_fixed_blocks(frame_len);
 #ifdef UFC_TUNING
-  if (const char* ab = std::getenv("UFC_ABLATE")) freeze |= std::atoi(ab);
+  if (const char* ab = std::getenv("UFC_ABLATE")) {
+    freeze |= std::atoi(ab);
+    lean = 0;
+  }
 #endif
   ufc_dev::KernelParams kp{};
   kp.bytes = d_frames;
@@ -251,6 +260,7 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
+  if (lean) return launch_lean_fixed(ctx, lean, false, kp, (hipStream_t)stream);
   return launch(ctx, cfg, freeze, kp, (hipStream_t)stream);
 }
 
@@ -284,6 +294,7 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
+  if (const int lean = lean_fixed_blocks(frame_len)) return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
   return launch(ctx, cfg, freeze | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
 
