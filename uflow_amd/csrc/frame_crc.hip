@@ -580,12 +580,50 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 // Lean kernel for fixed-length frames (frame_len >= 4, J = ceil((frame_len+4)/256) <= 6 blocks,
 // known at compile time): the batched gate of BASELINE.json configs 2 and 4.  Each wave owns a
 // balanced contiguous range of sets; loop-invariant geometry (front-fix masks, lane offsets) is
-// hoisted, set addresses are scalar, results gather with one select per set.
+// hoisted, set addresses are scalar, results gather with one select per set.  DEPTH sets are in
+// flight per wave (DEPTH-1 prefetched while one is computed); the first prefetches are issued
+// before the LDS tables are staged so that HBM is busy from the first cycle.
+// ABL (tuning builds only): kLeanAblLoads = loads + XOR fold, no CRC; kLeanAblCompute = CRC of
+// the prologue's registers, no loads in the loop.  Their results are meaningless.
 // ---------------------------------------------------------------------------------------------
-template <int J, bool SEAL>
+constexpr int kLeanAblLoads = 1;
+constexpr int kLeanAblCompute = 2;
+
+struct StageRegs {
+  uint32_t cv;
+  u32x4 n0, n1;
+};
+
+__device__ __forceinline__ StageRegs stage_load(const KernelParams& p) {
+  const int t = threadIdx.x;
+  StageRegs r;
+  r.cv = *as_global<g_u32>(p.chain_tab + t);
+  r.n0 = *as_global<g_u32x4>(p.nib_img + 8 * t);
+  r.n1 = *as_global<g_u32x4>(p.nib_img + 8 * t + 4);
+  return r;
+}
+
+// LDS writes of the staged tables, then a workgroup barrier that orders LDS only: data
+// prefetches issued before it stay in flight (no vmcnt(0) at the barrier).
+__device__ __forceinline__ void stage_store(const StageRegs& r, char* lds) {
+  const int t = threadIdx.x;
+  const uint32_t k = (uint32_t)t >> 8, e = (uint32_t)t & 255u;
+  const uint32_t cbase = kChainBase + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+  const u32x4 cr = {r.cv, r.cv, r.cv, r.cv};
+#pragma unroll
+  for (int i = 0; i < 8; i++) *(u32x4*)(lds + cbase + 16 * i) = cr;
+  *(u32x4*)(lds + 32 * t) = r.n0;
+  *(u32x4*)(lds + 32 * t + 16) = r.n1;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+template <int J, bool SEAL, int DEPTH, int ABL>
 __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParams p) {
+  static_assert(DEPTH == 2 || DEPTH == 3, "pipeline depth");
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-  stage_tables(p, lds);
+  const StageRegs sr = stage_load(p);
   Lane L;
   init_lane(L, lds, p.G);
 
@@ -598,9 +636,11 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
   const uint64_t s_begin = nsets * w / NW, s_end = nsets * (w + 1) / NW;
-  if (s_begin >= s_end) return;
-  // Sets before s_fast have a frame whose pad region precedes the buffer: slow path.
+  // Sets before s_fast have a frame whose pad region precedes the buffer: slow path.  With E =
+  // len the fast loads of a frame end exactly at its last byte, so no set at the end is unsafe.
   const uint64_t s_fast = ((uint64_t)pad + 4 * stride - 1) / (4 * stride);
+  const uint64_t s_main = max(s_begin, min(s_fast, s_end));
+  const bool have_main = s_main < s_end;
 
   // Loop invariants of this lane.
   const int64_t lane_off = (int64_t)L.grp * (int64_t)stride + 16 * L.col - pad;
@@ -622,44 +662,48 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
   }
   const uint32_t tmask = (L.col == 15) ? 0u : 0xFFFFFFFFu;  // zero the trailer word in the CRC
 
-  // frame results of the current run of 16 sets: lane (g, col=t) <- crc of frame 4t+g;
-  // lane 15 of group g collects valid bit t of frame 4t+g.
+  // Results of the current run of 16 sets: lane (g, col=t) <- crc of frame 4t+g; lane 15 of
+  // group g collects valid bit t of frame 4t+g.  Completed runs shift into hist_* registers and
+  // leave after the loop: a store inside the loop would make every later load wait vmcnt(0)
+  // (loads and stores share vmcnt and may complete out of order), draining the prefetch.
   uint32_t acc_crc = 0, acc_vbits = 0;
-  auto store_run = [&](uint64_t run_set0, int nset_in_run) {
+  uint32_t hist_crc[kLeanRuns], hist_vbits[kLeanRuns];
+#pragma unroll
+  for (int r = 0; r < kLeanRuns; r++) hist_crc[r] = hist_vbits[r] = 0;
+  auto write_trailer = [&](uint64_t f, uint32_t crc) {  // seal: BE32 CRC into the frame's trailer
+    uint8_t* a = p.wbytes + f * stride + n;
+    if (((uintptr_t)a & 3u) == 0) {
+      *as_global<g_u32w>((uint32_t*)a) = __builtin_bswap32(crc);
+    } else {
+      g_u8w* wp = as_global<g_u8w>(a);
+      wp[0] = (uint8_t)(crc >> 24);
+      wp[1] = (uint8_t)(crc >> 16);
+      wp[2] = (uint8_t)(crc >> 8);
+      wp[3] = (uint8_t)crc;
+    }
+  };
+  // Store one run (first set run_set0, nset sets): coalesced CRC words + valid bytes; seal mode
+  // writes the frames' trailers.
+  auto store_run = [&](uint64_t run_set0, int nset, uint32_t crcs, uint32_t vbits) {
     uint32_t vb = 0;
 #pragma unroll
     for (int g = 0; g < 4; g++) {
-      const uint32_t m = __builtin_amdgcn_readlane(acc_vbits, 16 * g + 15);
+      const uint32_t m = __builtin_amdgcn_readlane(vbits, 16 * g + 15);
       vb = (L.grp == g) ? m : vb;
     }
     const uint64_t f = (run_set0 + (uint64_t)L.col) * 4 + (uint64_t)L.grp;
-    if (L.col < nset_in_run && f < p.nframes) {
-      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = acc_crc;
+    if (L.col < nset && f < p.nframes) {
+      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crcs;
       if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)((vb >> L.col) & 1u);
+      if (SEAL) write_trailer(f, crcs);
     }
   };
-  // Finish set s (t = its index in the current run).
-  auto finish = [&](uint64_t s, int t, const Chains& c) {
-    const uint32_t crc = ~group_lin(L, c);
+  // Finish a set (t = its index in the current run).
+  auto finish = [&](int t, const Chains& c) {
+    const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
     acc_crc = (L.col == t) ? crc : acc_crc;
-    if (SEAL) {
-      const uint64_t f = s * 4 + (uint64_t)L.grp;
-      if (L.col == 15 && f < p.nframes) {
-        uint8_t* a = p.wbytes + f * stride + n;
-        if (((uintptr_t)a & 3u) == 0) {
-          *as_global<g_u32w>((uint32_t*)a) = __builtin_bswap32(crc);
-        } else {
-          g_u8w* wp = as_global<g_u8w>(a);
-          wp[0] = (uint8_t)(crc >> 24);
-          wp[1] = (uint8_t)(crc >> 16);
-          wp[2] = (uint8_t)(crc >> 8);
-          wp[3] = (uint8_t)crc;
-        }
-      }
-    } else {
-      const uint32_t ok = (len >= 5u && __builtin_bswap32(c.tr) == crc) ? 1u : 0u;
-      acc_vbits |= ok << t;  // meaningful in lane 15 of each group
-    }
+    const uint32_t ok = (len >= 5u && __builtin_bswap32(c.tr) == crc) ? 1u : 0u;
+    acc_vbits |= ok << t;  // meaningful in lane 15 of each group
   };
   // Frame-set processing from a loaded item (J blocks).
   auto compute = [&](const ItemBuf<J>& b, Chains& c) {
@@ -670,7 +714,13 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
         c.tr = x.w;
         x.w &= tmask;
       }
-      if (j == 0) {
+      if (ABL == kLeanAblLoads) {
+        if (j == 0) {
+          c.v0 = x.x; c.v1 = x.y; c.v2 = x.z; c.v3 = x.w;
+        } else {
+          c.v0 ^= x.x; c.v1 ^= x.y; c.v2 ^= x.z; c.v3 ^= x.w;
+        }
+      } else if (j == 0) {
         c.v0 = (x.x & dm[0]) | pre[0];
         c.v1 = (x.y & dm[1]) | pre[1];
         c.v2 = (x.z & dm[2]) | pre[2];
@@ -684,16 +734,105 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
       }
     }
   };
-  auto lane_ptr = [&](uint64_t s) -> const uint8_t* {
-    return p.bytes + s * 4 * stride + lane_off;  // s*4*stride is wave-uniform
+  // Lane load address of set ss.  The last set may hold frames past nframes: those lanes re-read
+  // frame nframes-1 (loads never leave the buffer) and their results are not stored.
+  auto safe_ptr = [&](uint64_t ss) -> const uint8_t* {
+    const uint64_t room = p.nframes - 1 - 4 * ss;  // >= 0 for every set < nsets
+    const int64_t over = (int64_t)L.grp - (int64_t)min(room, (uint64_t)3);
+    return p.bytes + ss * 4 * stride + lane_off - (over > 0 ? over * (int64_t)stride : 0);
+  };
+  uint64_t s = s_main;
+  auto load = [&](uint64_t ss, ItemBuf<J>& b) {
+    const uint8_t* q = safe_ptr(ss < s_end ? ss : s);  // past the range: re-read a safe set
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
+      b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
   };
 
-  uint64_t s = s_begin;
-  uint64_t run0 = s_begin;
-  // Edge sets: slow path (they are the first sets of the batch).
-  for (; s < s_end && s < s_fast; s++) {
-    const int t = (int)(s - run0);
-    FrameDesc d = make_desc(min(s * 4 + (uint64_t)L.grp, p.nframes - 1) * stride, len);
+  // Prologue prefetch, issued unconditionally (a wave without fast sets reads the nibble image,
+  // 32 KiB of valid memory): a load under a branch would make the wait-count merge at the barrier
+  // drain every outstanding load.
+  ItemBuf<J> A, B, C;
+  {
+    const uint8_t* q0 = have_main ? safe_ptr(s_main) : (const uint8_t*)p.nib_img + 16 * L.col;
+    const uint8_t* q1 = (have_main && s_main + 1 < s_end) ? safe_ptr(s_main + 1) : q0;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q0 + 256 * j));
+      A.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    if (DEPTH == 3) {
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q1 + 256 * j));
+        B.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    }
+  }
+  stage_store(sr, lds);
+
+  if (have_main) {
+    // Main loop over the fast sets [s_main, s_end) (at most 16 * kLeanRuns, host-chunked),
+    // DEPTH-deep, no stores.
+    uint64_t run0 = s_main;
+    Chains c{0u, 0u, 0u, 0u, 0u};
+    auto step = [&](ItemBuf<J>& cur, ItemBuf<J>& fill) {
+      if (ABL != kLeanAblCompute) load(s + (DEPTH - 1), fill);
+      compute(cur, c);
+      const int t = (int)(s - run0);
+      finish(t, c);
+      s++;
+      if (t == kSetsPerRun - 1 || s == s_end) {
+#pragma unroll
+        for (int r = kLeanRuns - 1; r > 0; r--) {
+          hist_crc[r] = hist_crc[r - 1];
+          hist_vbits[r] = hist_vbits[r - 1];
+        }
+        hist_crc[0] = acc_crc;
+        hist_vbits[0] = acc_vbits;
+        run0 = s;
+        acc_vbits = 0;
+      }
+    };
+    // Whole rounds of DEPTH steps with one uniform trip test, then the remainder: early exits
+    // inside the round would merge into the loop latch and the wait-count state at the loop
+    // header would include the exit paths' fresh loads (vmcnt(0) every round).
+    if (DEPTH == 2) {
+      while (s + 2 <= s_end) {
+        step(A, B);
+        step(B, A);
+      }
+      if (s < s_end) step(A, B);
+    } else {
+      while (s + 3 <= s_end) {
+        step(A, C);
+        step(B, A);
+        step(C, B);
+      }
+      if (s < s_end) step(A, C);
+      if (s < s_end) step(B, A);
+    }
+    // hist[r] holds run nruns-1-r; runs start every 16 sets from s_main.
+    const uint64_t nsets_main = s_end - s_main;
+    const int nruns = (int)((nsets_main + kSetsPerRun - 1) / kSetsPerRun);
+#pragma unroll
+    for (int r = 0; r < kLeanRuns; r++) {
+      const int q = nruns - 1 - r;
+      if (q >= 0) {
+        const uint64_t first = s_main + (uint64_t)q * kSetsPerRun;
+        const int cnt = (int)min((uint64_t)kSetsPerRun, s_end - first);
+        store_run(first, cnt, hist_crc[r], hist_vbits[r]);
+      }
+    }
+  }
+
+  // Edge sets [s_begin, s_main) (the first sets of the batch only): byte loads restricted to the
+  // frame, results stored per set by lane 15 of each group.
+#pragma unroll 1
+  for (uint64_t e = s_begin; e < s_main; e++) {
+    FrameDesc d = make_desc(min(e * 4 + (uint64_t)L.grp, p.nframes - 1) * stride, len);
     Chains c{0u, 0u, 0u, 0u, 0u};
 #pragma unroll 1
     for (int blk = 0; blk < J; blk++) {
@@ -711,76 +850,52 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
       }
       process_block<false>(L, d, blk, make_uint4(wv[0], wv[1], wv[2], wv[3]), c);
     }
-    finish(s, t, c);
-    if (t == kSetsPerRun - 1 || s + 1 == s_end) {
-      store_run(run0, t + 1);
-      run0 = s + 1;
-      acc_vbits = 0;
-    }
-  }
-  if (s >= s_end) return;
-  // The last set may hold frames past nframes: those lanes re-read frame nframes-1 (loads never
-  // leave the buffer) and their results are not stored.  Only the final set pays the clamp.
-  auto safe_ptr = [&](uint64_t ss) -> const uint8_t* {
-    const uint64_t room = p.nframes - 1 - 4 * ss;  // >= 0 for every set < nsets
-    const int64_t over = (int64_t)L.grp - (int64_t)min(room, (uint64_t)3);
-    return lane_ptr(ss) - (over > 0 ? over * (int64_t)stride : 0);
-  };
-
-  // Main loop: double-buffered over sets.
-  Chains c{0u, 0u, 0u, 0u, 0u};
-  auto load = [&](uint64_t ss, ItemBuf<J>& b) {
-    const uint8_t* q = safe_ptr(ss < s_end ? ss : s);
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
-      b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-  };
-  auto step = [&](ItemBuf<J>& cur, ItemBuf<J>& nxt) -> bool {
-    load(s + 1, nxt);
-    compute(cur, c);
-    const int t = (int)(s - run0);
-    finish(s, t, c);
-    s++;
-    if (t == kSetsPerRun - 1 || s == s_end) {
-      store_run(run0, t + 1);
-      run0 = s;
-      acc_vbits = 0;
-    }
-    return s < s_end;
-  };
-  {
-    ItemBuf<J> A, B;
-    load(s, A);
-    while (step(A, B) && step(B, A)) {
+    acc_vbits = 0;
+    finish(15, c);  // lane 15 of each group receives the crc and (bit 15) the valid flag
+    const uint64_t f = e * 4 + (uint64_t)L.grp;
+    if (L.col == 15 && f < p.nframes) {
+      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = acc_crc;
+      if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)((acc_vbits >> 15) & 1u);
+      if (SEAL) write_trailer(f, acc_crc);
     }
   }
 }
 
-template __global__ void frame_crc_fixed_kernel<1, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<2, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<3, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<4, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<5, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<1, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<2, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<3, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<4, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<5, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, true>(const KernelParams);
+#define UFC_INST_FIXED(J)                                                                \
+  template __global__ void frame_crc_fixed_kernel<J, false, 2, 0>(const KernelParams);   \
+  template __global__ void frame_crc_fixed_kernel<J, true, 2, 0>(const KernelParams);    \
+  template __global__ void frame_crc_fixed_kernel<J, false, 3, 0>(const KernelParams);   \
+  template __global__ void frame_crc_fixed_kernel<J, true, 3, 0>(const KernelParams);
+UFC_INST_FIXED(1) UFC_INST_FIXED(2) UFC_INST_FIXED(3) UFC_INST_FIXED(4) UFC_INST_FIXED(5) UFC_INST_FIXED(6)
 
-const void* fixed_kernel_symbol(int J, bool seal) {
-  switch (J) {
-    case 1: return seal ? (const void*)frame_crc_fixed_kernel<1, true> : (const void*)frame_crc_fixed_kernel<1, false>;
-    case 2: return seal ? (const void*)frame_crc_fixed_kernel<2, true> : (const void*)frame_crc_fixed_kernel<2, false>;
-    case 3: return seal ? (const void*)frame_crc_fixed_kernel<3, true> : (const void*)frame_crc_fixed_kernel<3, false>;
-    case 4: return seal ? (const void*)frame_crc_fixed_kernel<4, true> : (const void*)frame_crc_fixed_kernel<4, false>;
-    case 5: return seal ? (const void*)frame_crc_fixed_kernel<5, true> : (const void*)frame_crc_fixed_kernel<5, false>;
-    case 6: return seal ? (const void*)frame_crc_fixed_kernel<6, true> : (const void*)frame_crc_fixed_kernel<6, false>;
-    default: return nullptr;
+#ifdef UFC_TUNING
+template __global__ void frame_crc_fixed_kernel<6, false, 2, kLeanAblLoads>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 2, kLeanAblCompute>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute>(const KernelParams);
+#endif
+
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl) {
+  if (depth != 2 && depth != 3) return nullptr;
+#define UFC_PICK_FIXED(JJ)                                                                                  \
+  if (J == JJ && abl == 0) {                                                                                \
+    if (depth == 2) return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 2, 0>                      \
+                                : (const void*)frame_crc_fixed_kernel<JJ, false, 2, 0>;                    \
+    return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0> : (const void*)frame_crc_fixed_kernel<JJ, false, 3, 0>; \
   }
+  UFC_PICK_FIXED(1) UFC_PICK_FIXED(2) UFC_PICK_FIXED(3) UFC_PICK_FIXED(4) UFC_PICK_FIXED(5) UFC_PICK_FIXED(6)
+#undef UFC_PICK_FIXED
+#ifdef UFC_TUNING
+  if (J == 6 && !seal) {
+    if (abl == kLeanAblLoads)
+      return depth == 2 ? (const void*)frame_crc_fixed_kernel<6, false, 2, kLeanAblLoads>
+                        : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads>;
+    if (abl == kLeanAblCompute)
+      return depth == 2 ? (const void*)frame_crc_fixed_kernel<6, false, 2, kLeanAblCompute>
+                        : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute>;
+  }
+#endif
+  return nullptr;
 }
 
 #define UFC_INST_MODES(JC)                                                                          \

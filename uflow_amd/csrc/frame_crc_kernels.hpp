@@ -32,7 +32,12 @@ struct KernelParams {
 const void* kernel_symbol(int jc, int mode);
 bool config_available(int jc);
 // Lean fixed-length kernel (frame_len >= 4, J = ceil((frame_len + 4) / 256) in 1..6); one
-// workgroup per CU, each wave a balanced contiguous range of 4-frame sets.
-const void* fixed_kernel_symbol(int J, bool seal);
+// workgroup per CU, each wave a balanced contiguous range of 4-frame sets, `depth` (2 or 3) sets
+// in flight per wave.  abl != 0 selects the ablation variants of tuning builds (J = 6 only).
+constexpr int kLeanDepthDefault = 3;
+// Results stay in registers until a wave's range is done: at most 16 * kLeanRuns sets per wave,
+// i.e. a launch covers at most (waves in the grid) * 16 * kLeanRuns * 4 frames (host-chunked).
+constexpr int kLeanRuns = 8;
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl);
 
 }  // namespace ufc_dev

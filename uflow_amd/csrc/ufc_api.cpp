@@ -4,6 +4,7 @@
 // frame_crc.hip.  Batched calls never fall back to the CPU.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -100,20 +101,37 @@ int lean_fixed_blocks(uint64_t frame_len) {
 }
 
 int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal);
+  int depth = ufc_dev::kLeanDepthDefault, abl = 0;
+  if (const char* d = std::getenv("UFC_LEAN_DEPTH")) depth = std::atoi(d);
+#ifdef UFC_TUNING
+  if (const char* ab = std::getenv("UFC_LEAN_ABL"); ab && !seal) abl = std::atoi(ab);
+#endif
+  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl);
   if (!fn) return UFC_ERR_INVALID_ARG;
-  // Each wave takes a balanced contiguous range of sets; no more waves than sets.
-  const uint64_t nsets = (kp.nframes + 3) / 4;
-  const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
-  uint64_t blocks = (nsets + waves_per_block - 1) / waves_per_block;
-  if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
-  if (blocks < 1) blocks = 1;
   kp.chain_tab = ctx->d_chain;
   kp.nib_img = ctx->d_nib;
   kp.G = ctx->G;
-  void* args[] = {&kp};
-  hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
-  if (e != hipSuccess) return hip_fail(ctx, e);
+  // One 1024-thread workgroup per CU; a wave's results stay in registers, so one launch covers
+  // at most 16 * kLeanRuns sets per wave: larger batches go in chunks (every frame in a chunk
+  // keeps its absolute address, so only the first sets of a chunk take the edge path).
+  const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
+  const uint64_t chunk = (uint64_t)ctx->ncu * waves_per_block * 16 * ufc_dev::kLeanRuns * 4;
+  const uint64_t total = kp.nframes;
+  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
+    ufc_dev::KernelParams c = kp;
+    c.nframes = std::min(chunk, total - f0);
+    c.bytes = kp.bytes + f0 * kp.stride;
+    if (kp.wbytes) c.wbytes = kp.wbytes + f0 * kp.stride;
+    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
+    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
+    const uint64_t nsets = (c.nframes + 3) / 4;
+    uint64_t blocks = (nsets + waves_per_block - 1) / waves_per_block;
+    if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
+    if (blocks < 1) blocks = 1;
+    void* args[] = {&c};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+  }
   return UFC_OK;
 }
 
