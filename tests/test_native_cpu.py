@@ -1,0 +1,119 @@
+"""CPU: the C-ABI library (libuflowcrc.so) loads and exports every symbol include/uflow_frame_crc.h
+declares; its host entry points (ufc_crc32_compute/extend, ufc_frame_validate/seal -- the scalar
+drop-ins for crc::compute / crc::extend and the Frame::read CRC gate) agree with the oracle and the
+golden data; argument checking and error codes behave as documented.  No GPU compute here.
+"""
+import ctypes
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle
+from uflow_amd import _native, crc
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "uflow_frame_crc.h")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def header_symbols():
+    with open(HEADER) as f:
+        text = f.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ufc_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_header_symbol():
+    syms = header_symbols()
+    assert "ufc_crc_batch_fixed" in syms and "ufc_validate_host_varlen" in syms, syms
+    l = ctypes.CDLL(_native.LIB_PATH)
+    missing = [s for s in syms if not hasattr(l, s)]
+    assert not missing, missing
+    assert set(syms) == set(_native.SYMBOLS), "header vs ctypes binding differ"
+
+
+def test_constants_match_header():
+    with open(HEADER) as f:
+        text = f.read()
+    consts = dict(re.findall(r"#define\s+(UFC_\w+)\s+\(?(-?\d+)\)?", text))
+    assert int(consts["UFC_FRAME_CRC_SIZE"]) == crc.FRAME_CRC_SIZE == 4
+    assert int(consts["UFC_FRAME_OVERHEAD"]) == crc.FRAME_OVERHEAD == 5
+    assert int(consts["UFC_MAX_FRAME_SIZE"]) == crc.MAX_FRAME_SIZE == 1472
+    assert int(consts["UFC_OK"]) == _native.UFC_OK == 0
+
+
+def test_host_kat_and_lengths():
+    assert crc.compute(b"123456789") == 0x11A6F2A3
+    assert crc.extend(0, b"123456789") == 0x11A6F2A3
+    assert crc.compute(b"\x00") != 0
+    with open(os.path.join(GOLDEN, "crc_lengths.json")) as f:
+        g = json.load(f)
+    for n, c in g["ramp"]:
+        assert crc.compute(bytes(i % 256 for i in range(n))) == int(c, 16)
+
+
+def test_host_extend_random_inits_vs_oracle():
+    rng = np.random.default_rng(8)
+    for _ in range(200):
+        data = rng.integers(0, 256, size=int(rng.integers(0, 2000)), dtype=np.uint8).tobytes()
+        init = int(rng.integers(0, 2**32))
+        assert crc.extend(init, data) == oracle.extend_slow(init, data)
+
+
+def test_host_gate_on_reference_frames():
+    with open(os.path.join(GOLDEN, "frames.json")) as f:
+        frames = json.load(f)["frames"]
+    for fr in frames:
+        b = bytes.fromhex(fr["hex"])
+        assert crc.frame_validate(b), fr["name"]
+        assert not crc.frame_validate(b + b"\x00")
+        for i in range(0, len(b)):
+            assert not crc.frame_validate(b[:i])
+        bb = bytearray(b)
+        bb[-4:] = b"\0\0\0\0"
+        assert crc.frame_seal(bb) == int(fr["crc"], 16)
+        assert bytes(bb) == b
+
+
+def test_host_gate_random_fixture():
+    z = np.load(os.path.join(GOLDEN, "random_frames.npz"))
+    data, off = z["data"], z["offsets"]
+    for i in range(len(off) - 1):
+        fb = data[int(off[i]):int(off[i + 1])].tobytes()
+        assert crc.frame_validate(fb) == bool(z["valid"][i])
+
+
+def test_seal_rejects_short_frames():
+    l = _native.lib()
+    buf = (ctypes.c_uint8 * 3)()
+    assert l.ufc_frame_seal(buf, 3) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_frame_validate(None, 10) == 0
+    assert l.ufc_frame_seal(None, 10) == _native.UFC_ERR_INVALID_ARG
+
+
+def test_batch_entry_points_reject_bad_args_without_gpu():
+    l = _native.lib()
+    null = ctypes.c_void_p()
+    assert l.ufc_crc_batch_fixed(null, None, 0, 0, 1, None, None, None) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_crc_batch_varlen(null, None, None, 1, None, None, None) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_seal_batch_fixed(null, None, 0, 0, 1, None, None) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_seal_batch_varlen(null, None, None, 1, None, None) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_ctx_create(None, 0) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_ctx_destroy(null) == _native.UFC_OK
+    for code in (0, -1, -2, -3, -4, -99):
+        assert l.ufc_error_string(code)
+
+
+def test_ctx_create_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    ctx = ctypes.c_void_p()
+    rc = _native.lib().ufc_ctx_create(ctypes.byref(ctx), 0)
+    assert rc in (_native.UFC_ERR_NO_DEVICE, _native.UFC_ERR_HIP)
+    from uflow_amd.batch import FrameCrcEngine
+    with pytest.raises(_native.NativeError):
+        FrameCrcEngine(0)

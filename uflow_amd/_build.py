@@ -23,8 +23,9 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build_native(force=False, verbose=False, tuning=False, out=None):
-    """tuning=True adds the ablation kernels (-DUFC_TUNING) and writes to `out` instead."""
+def build_native(force=False, verbose=False, tuning=False, out=None, defines=()):
+    """tuning=True adds the ablation kernels (-DUFC_TUNING); `defines` adds -D flags (tuning
+    experiments).  Both are meant with `out` pointing away from the product library."""
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
     deps.append(os.path.join(REPO_DIR, "include", "uflow_frame_crc.h"))
     target = out or LIB_PATH
@@ -34,6 +35,8 @@ def build_native(force=False, verbose=False, tuning=False, out=None):
            "-o", target + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
     if tuning:
         cmd.insert(1, "-DUFC_TUNING")
+    for d in defines:
+        cmd.insert(1, "-D" + d)
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

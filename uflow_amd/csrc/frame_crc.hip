@@ -586,6 +586,31 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 // ABL (tuning builds only): kLeanAblLoads = loads + XOR fold, no CRC; kLeanAblCompute = CRC of
 // the prologue's registers, no loads in the loop.  Their results are meaningless.
 // ---------------------------------------------------------------------------------------------
+#ifndef UFC_LEAN_NT
+// Cache policy of the frame loads: 1 = all non-temporal (streaming); 0 = all default;
+// 2 = default for the first and last block of a frame (their boundary lines are shared with the
+// neighbouring frames and re-read shortly after), non-temporal for the blocks in between.
+#define UFC_LEAN_NT 1
+#endif
+template <bool NT>
+__device__ __forceinline__ uint4 load_frame16(const uint8_t* q) {
+  u32x4 v;
+  if constexpr (NT)
+    v = __builtin_nontemporal_load(as_global<g_u32x4>(q));
+  else
+    v = *as_global<g_u32x4>(q);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// One set's J blocks for this lane (lane address q = block 0).
+template <int J>
+__device__ __forceinline__ void load_set(const uint8_t* q, ItemBuf<J>& b) {
+  constexpr bool kEdgeNT = UFC_LEAN_NT == 1, kMidNT = UFC_LEAN_NT != 0;
+  b.x[0] = load_frame16<kEdgeNT>(q);
+#pragma unroll
+  for (int j = 1; j < J - 1; j++) b.x[j] = load_frame16<kMidNT>(q + 256 * j);
+  if constexpr (J > 1) b.x[J - 1] = load_frame16<kEdgeNT>(q + 256 * (J - 1));
+}
+
 constexpr int kLeanAblLoads = 1;
 constexpr int kLeanAblCompute = 2;
 
@@ -705,11 +730,15 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
     const uint32_t ok = (len >= 5u && __builtin_bswap32(c.tr) == crc) ? 1u : 0u;
     acc_vbits |= ok << t;  // meaningful in lane 15 of each group
   };
+  uint64_t s = s_main;  // next set of the main loop
   // Frame-set processing from a loaded item (J blocks).
   auto compute = [&](const ItemBuf<J>& b, Chains& c) {
 #pragma unroll
     for (int j = 0; j < J; j++) {
       uint4 x = b.x[j];
+      if (ABL == kLeanAblCompute && j == 0) {  // not loop-invariant
+        x.x ^= (uint32_t)s; x.y ^= (uint32_t)s; x.z ^= (uint32_t)s; x.w ^= (uint32_t)s;
+      }
       if (j == J - 1) {
         c.tr = x.w;
         x.w &= tmask;
@@ -741,14 +770,9 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
     const int64_t over = (int64_t)L.grp - (int64_t)min(room, (uint64_t)3);
     return p.bytes + ss * 4 * stride + lane_off - (over > 0 ? over * (int64_t)stride : 0);
   };
-  uint64_t s = s_main;
   auto load = [&](uint64_t ss, ItemBuf<J>& b) {
     const uint8_t* q = safe_ptr(ss < s_end ? ss : s);  // past the range: re-read a safe set
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
-      b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-    }
+    load_set<J>(q, b);
   };
 
   // Prologue prefetch, issued unconditionally (a wave without fast sets reads the nibble image,
@@ -758,18 +782,8 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
   {
     const uint8_t* q0 = have_main ? safe_ptr(s_main) : (const uint8_t*)p.nib_img + 16 * L.col;
     const uint8_t* q1 = (have_main && s_main + 1 < s_end) ? safe_ptr(s_main + 1) : q0;
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q0 + 256 * j));
-      A.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-    if (DEPTH == 3) {
-#pragma unroll
-      for (int j = 0; j < J; j++) {
-        const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q1 + 256 * j));
-        B.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-      }
-    }
+    load_set<J>(q0, A);
+    if (DEPTH == 3) load_set<J>(q1, B);
   }
   stage_store(sr, lds);
 
