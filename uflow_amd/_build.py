@@ -31,7 +31,10 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
     target = out or LIB_PATH
     if not force and not _stale(target, deps):
         return target
+    # No atomic optimizer: the lean kernel's single-lane claim atomics must stay plain
+    # global_atomic_add (the optimizer reads the result back at once, forcing a vmcnt(0) wait).
     cmd = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17", "-Wall",
+           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
            "-o", target + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
     if tuning:
         cmd.insert(1, "-DUFC_TUNING")

@@ -644,10 +644,18 @@ __device__ __forceinline__ void stage_store(const StageRegs& r, char* lds) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <int J, bool SEAL, int DEPTH, int ABL>
+// Per-workgroup claim counters of the dynamic schedule (kCtrWordsPerBlock words per workgroup,
+// one 128-byte line each): [0] = claims handed out, [1] = waves finished.  The last wave of a
+// workgroup to finish resets both, so every launch finds them zero (launches of one slot are
+// stream-ordered; see ufc_api.cpp).
+
+template <int J, bool SEAL, int DEPTH, int ABL, bool DYN>
 __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParams p) {
-  static_assert(DEPTH == 2 || DEPTH == 3, "pipeline depth");
+  static_assert(DEPTH == 2 || DEPTH == 3, "pipeline depth (4 spills at J = 6)");
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+#ifdef UFC_TUNING
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   const StageRegs sr = stage_load(p);
   Lane L;
   init_lane(L, lds, p.G);
@@ -656,16 +664,47 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
   const uint32_t len = (uint32_t)p.frame_len;  // >= 4 (host checks)
   const uint32_t n = len - 4u;
   const int pad = J * 256 - (int)len;          // E = len
-  const uint64_t nsets = (p.nframes + 3) >> 2;
-  const uint64_t NW = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint32_t nsets = (uint32_t)((p.nframes + 3) >> 2);  // < 2^32 (host chunks launches)
+  const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wid;
-  const uint64_t s_begin = nsets * w / NW, s_end = nsets * (w + 1) / NW;
-  // Sets before s_fast have a frame whose pad region precedes the buffer: slow path.  With E =
-  // len the fast loads of a frame end exactly at its last byte, so no set at the end is unsafe.
-  const uint64_t s_fast = ((uint64_t)pad + 4 * stride - 1) / (4 * stride);
-  const uint64_t s_main = max(s_begin, min(s_fast, s_end));
-  const bool have_main = s_main < s_end;
+  const uint32_t w = blockIdx.x * wpb + wid;  // global wave index
+  // Sets before s_fast have a frame whose pad region precedes the buffer: they take the slow path
+  // (global wave 0, before its main loop).  front_ok: bytes before the batch are readable (a
+  // later chunk of a larger batch), so there are none.  With E = len the fast loads of a frame end exactly at
+  // its last byte, so no set at the end of the batch is unsafe.
+  const uint32_t s_fast =
+      p.front_ok ? 0u : (uint32_t)min(((uint64_t)pad + 4 * stride - 1) / (4 * stride), (uint64_t)nsets);
+  const uint32_t nfast = nsets - s_fast;
+  // This wave's set sequence q0 < q1 < q2 < ... (strictly increasing, so once one is past `q_end`
+  // all later ones are).  Static: a balanced contiguous range per wave.  Dynamic: the workgroup
+  // owns a contiguous range; wave i starts with sets lo+i (and lo+16+i at depth 3), then claims
+  // the following ones with a per-workgroup counter, so the 16 waves finish together whatever the SIMD arbitration does
+  // (oldest-wave-first arbitration otherwise finishes a CU's waves in four staggered groups).
+  uint32_t q_lo, q_end, q_cur, q_nx1, q_nx2;
+  if (DYN) {
+    q_lo = s_fast + (uint32_t)((uint64_t)nfast * blockIdx.x / gridDim.x);
+    q_end = s_fast + (uint32_t)((uint64_t)nfast * (blockIdx.x + 1) / gridDim.x);
+    q_cur = q_lo + wid;
+    q_nx1 = q_lo + wpb + wid;
+  } else {
+    const uint32_t NW = gridDim.x * wpb;
+    q_lo = s_fast + (uint32_t)((uint64_t)nfast * w / NW);
+    q_end = s_fast + (uint32_t)((uint64_t)nfast * (w + 1) / NW);
+    q_cur = q_lo;
+    q_nx1 = q_lo + 1;
+  }
+  uint32_t* ctr = DYN ? p.ctr + blockIdx.x * kCtrWordsPerBlock : nullptr;
+  // Claim the next set (lane 0 only; no atomic optimizer, see _build.py), consumed later with a
+  // counted wait: the claim is issued before a step's prefetch and read after its compute.
+  auto claim_issue = [&]() -> uint32_t {
+    uint32_t v = 0;  // (initialised: an undefined value would let the compiler drop the lane test)
+    if (L.lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  // (the first DEPTH - 1 sets of each wave are static: lo + i, lo + 16 + i)
+  auto claim_set = [&](uint32_t v) -> uint32_t {
+    return q_lo + (DEPTH - 1) * wpb + __builtin_amdgcn_readfirstlane(v);
+  };
 
   // Loop invariants of this lane.
   const int64_t lane_off = (int64_t)L.grp * (int64_t)stride + 16 * L.col - pad;
@@ -687,14 +726,15 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
   }
   const uint32_t tmask = (L.col == 15) ? 0u : 0xFFFFFFFFu;  // zero the trailer word in the CRC
 
-  // Results of the current run of 16 sets: lane (g, col=t) <- crc of frame 4t+g; lane 15 of
-  // group g collects valid bit t of frame 4t+g.  Completed runs shift into hist_* registers and
-  // leave after the loop: a store inside the loop would make every later load wait vmcnt(0)
-  // (loads and stores share vmcnt and may complete out of order), draining the prefetch.
-  uint32_t acc_crc = 0, acc_vbits = 0;
-  uint32_t hist_crc[kLeanRuns], hist_vbits[kLeanRuns];
+  // Results of the current run of 16 processed sets: lane (g, col=t) <- crc, and set index | valid
+  // << 31, of the run's t-th set, frame g.  Completed runs shift into hist_* registers and leave
+  // after the loop: a store inside the loop would make every later load wait vmcnt(0) (loads and
+  // stores share vmcnt and may complete out of order).
+  uint32_t acc_crc = 0, acc_qv = 0;
+  uint32_t hist_crc[kLeanRuns], hist_qv[kLeanRuns];
 #pragma unroll
-  for (int r = 0; r < kLeanRuns; r++) hist_crc[r] = hist_vbits[r] = 0;
+  for (int r = 0; r < kLeanRuns; r++) hist_crc[r] = hist_qv[r] = 0;
+  uint32_t t = 0, nhist = 0;  // sets in the current run, completed runs held (uniform)
   auto write_trailer = [&](uint64_t f, uint32_t crc) {  // seal: BE32 CRC into the frame's trailer
     uint8_t* a = p.wbytes + f * stride + n;
     if (((uintptr_t)a & 3u) == 0) {
@@ -707,37 +747,56 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
       wp[3] = (uint8_t)crc;
     }
   };
-  // Store one run (first set run_set0, nset sets): coalesced CRC words + valid bytes; seal mode
+  // Store one run (cnt sets): per lane the CRC word and valid byte of frame 4*q + g; seal mode
   // writes the frames' trailers.
-  auto store_run = [&](uint64_t run_set0, int nset, uint32_t crcs, uint32_t vbits) {
-    uint32_t vb = 0;
-#pragma unroll
-    for (int g = 0; g < 4; g++) {
-      const uint32_t m = __builtin_amdgcn_readlane(vbits, 16 * g + 15);
-      vb = (L.grp == g) ? m : vb;
-    }
-    const uint64_t f = (run_set0 + (uint64_t)L.col) * 4 + (uint64_t)L.grp;
-    if (L.col < nset && f < p.nframes) {
+  auto store_run = [&](int cnt, uint32_t crcs, uint32_t qv) {
+    const uint64_t f = (uint64_t)(qv & 0x7FFFFFFFu) * 4 + (uint64_t)L.grp;
+    if (L.col < cnt && f < p.nframes) {
       if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crcs;
-      if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)((vb >> L.col) & 1u);
+      if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)(qv >> 31);
       if (SEAL) write_trailer(f, crcs);
     }
   };
-  // Finish a set (t = its index in the current run).
-  auto finish = [&](int t, const Chains& c) {
-    const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
-    acc_crc = (L.col == t) ? crc : acc_crc;
-    const uint32_t ok = (len >= 5u && __builtin_bswap32(c.tr) == crc) ? 1u : 0u;
-    acc_vbits |= ok << t;  // meaningful in lane 15 of each group
+  auto store_hist = [&]() {
+#pragma unroll
+    for (int r = 0; r < kLeanRuns; r++)
+      if ((uint32_t)r < nhist) store_run(kSetsPerRun, hist_crc[r], hist_qv[r]);
   };
-  uint64_t s = s_main;  // next set of the main loop
+  // Finish set q (this run's t-th): the trailer word (lane 15 of the frame's row) is broadcast to
+  // the row (DPP row_newbcast:15), so every lane of the frame has its validity.
+  auto finish = [&](uint32_t q, const Chains& c) {
+    const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
+    const uint32_t ok = (len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
+    acc_crc = (L.col == (int)t) ? crc : acc_crc;
+    acc_qv = (L.col == (int)t) ? (q | (ok << 31)) : acc_qv;
+    if (++t == kSetsPerRun) {
+      // shift the run into the history (hist[0] newest); a full history is stored first, followed
+      // by an explicit vmcnt(0) so that no store stays pending into the loop (rare: > 128 sets
+      // per wave in one launch).
+      if (nhist == kLeanRuns) {
+        store_hist();
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+        nhist = 0;
+      }
+#pragma unroll
+      for (int r = kLeanRuns - 1; r > 0; r--) {
+        hist_crc[r] = hist_crc[r - 1];
+        hist_qv[r] = hist_qv[r - 1];
+      }
+      hist_crc[0] = acc_crc;
+      hist_qv[0] = acc_qv;
+      nhist++;
+      t = 0;
+    }
+  };
   // Frame-set processing from a loaded item (J blocks).
-  auto compute = [&](const ItemBuf<J>& b, Chains& c) {
+  auto compute = [&](uint32_t q, const ItemBuf<J>& b, Chains& c) {
 #pragma unroll
     for (int j = 0; j < J; j++) {
       uint4 x = b.x[j];
       if (ABL == kLeanAblCompute && j == 0) {  // not loop-invariant
-        x.x ^= (uint32_t)s; x.y ^= (uint32_t)s; x.z ^= (uint32_t)s; x.w ^= (uint32_t)s;
+        x.x ^= q; x.y ^= q; x.z ^= q; x.w ^= q;
       }
       if (j == J - 1) {
         c.tr = x.w;
@@ -763,150 +822,185 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
       }
     }
   };
-  // Lane load address of set ss.  The last set may hold frames past nframes: those lanes re-read
-  // frame nframes-1 (loads never leave the buffer) and their results are not stored.
-  auto safe_ptr = [&](uint64_t ss) -> const uint8_t* {
-    const uint64_t room = p.nframes - 1 - 4 * ss;  // >= 0 for every set < nsets
-    const int64_t over = (int64_t)L.grp - (int64_t)min(room, (uint64_t)3);
-    return p.bytes + ss * 4 * stride + lane_off - (over > 0 ? over * (int64_t)stride : 0);
+  // Lane load address of set q.  The last set may hold frames past nframes; those lanes re-read
+  // frame nframes-1 (loads never leave the buffer) and their results are not stored.  A set past
+  // the wave's range (prefetches of the final round, claims past the end) reads the nibble image
+  // instead: 32 KiB of valid, L2-resident memory, so it costs no HBM traffic.
+  auto lane_ptr = [&](uint32_t q) -> const uint8_t* {
+    const uint32_t qc = min(q, nsets - 1);
+    const uint32_t room = (uint32_t)(p.nframes - 1 - 4 * (uint64_t)qc);
+    const int64_t over = (int64_t)L.grp - (int64_t)min(room, 3u);
+    const uint8_t* a = p.bytes + (uint64_t)qc * 4 * stride + lane_off - (over > 0 ? over * (int64_t)stride : 0);
+    return q < q_end ? a : (const uint8_t*)p.nib_img + 16 * L.col;
   };
-  auto load = [&](uint64_t ss, ItemBuf<J>& b) {
-    const uint8_t* q = safe_ptr(ss < s_end ? ss : s);  // past the range: re-read a safe set
-    load_set<J>(q, b);
-  };
+  auto load = [&](uint32_t q, ItemBuf<J>& b) { load_set<J>(lane_ptr(q), b); };
 
-  // Prologue prefetch, issued unconditionally (a wave without fast sets reads the nibble image,
-  // 32 KiB of valid memory): a load under a branch would make the wait-count merge at the barrier
-  // drain every outstanding load.
+  // Prologue: claim (dynamic), first prefetches, then the LDS tables: HBM is busy from the start.
+  // Depth 3 keeps q_cur and q_nx1 in flight and loads q_nx2 in the first step; depth 2 keeps
+  // q_cur in flight and loads q_nx1 (static in both schedules) in the first step.
+  // Claims are read two steps after they are issued (ring cX/cY/cZ): reading a claim waits, in
+  // vmcnt order, for every load issued before it, so it must be older than the loads of the set
+  // about to be computed.  The prologue issues the claims read in steps 0 and 1.
   ItemBuf<J> A, B, C;
-  {
-    const uint8_t* q0 = have_main ? safe_ptr(s_main) : (const uint8_t*)p.nib_img + 16 * L.col;
-    const uint8_t* q1 = (have_main && s_main + 1 < s_end) ? safe_ptr(s_main + 1) : q0;
-    load_set<J>(q0, A);
-    if (DEPTH == 3) load_set<J>(q1, B);
+  uint32_t cX = 0, cY = 0, cZ = 0;
+  if (DYN) {
+    cY = claim_issue();
+    cZ = claim_issue();
   }
+  load(q_cur, A);
+  if (DEPTH == 3) load(q_nx1, B);
   stage_store(sr, lds);
+#ifdef UFC_TUNING
+  const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
+#endif
+  q_nx2 = (DEPTH == 3 && !DYN) ? q_lo + 2 : 0;
 
-  if (have_main) {
-    // Main loop over the fast sets [s_main, s_end) (at most 16 * kLeanRuns, host-chunked),
-    // DEPTH-deep, no stores.
-    uint64_t run0 = s_main;
-    Chains c{0u, 0u, 0u, 0u, 0u};
-    auto step = [&](ItemBuf<J>& cur, ItemBuf<J>& fill) {
-      if (ABL != kLeanAblCompute) load(s + (DEPTH - 1), fill);
-      compute(cur, c);
-      const int t = (int)(s - run0);
-      finish(t, c);
-      s++;
-      if (t == kSetsPerRun - 1 || s == s_end) {
+  // Edge sets [0, s_fast) (the first sets of the batch only): global wave 0, before its main
+  // loop (the dynamic schedule rebalances), byte loads restricted to the frame, results stored
+  // per set by lane 15 of each group, then an explicit vmcnt(0) so that no store stays pending
+  // into the loop.
+  if (w == 0 && s_fast > 0) {
+#pragma unroll 1
+    for (uint32_t e = 0; e < s_fast; e++) {
+      FrameDesc d = make_desc(min((uint64_t)e * 4 + (uint64_t)L.grp, p.nframes - 1) * stride, len);
+      Chains ce{0u, 0u, 0u, 0u, 0u};
+#pragma unroll 1
+      for (int blk = 0; blk < J; blk++) {
+        uint32_t wv[4];
 #pragma unroll
-        for (int r = kLeanRuns - 1; r > 0; r--) {
-          hist_crc[r] = hist_crc[r - 1];
-          hist_vbits[r] = hist_vbits[r - 1];
+        for (int b = 0; b < 4; b++) {
+          const int o = 256 * blk + 16 * L.col + 4 * b - d.pad;
+          uint32_t a = 0;
+#pragma unroll 1
+          for (int k = 0; k < 4; k++) {
+            const int ob = o + k;
+            if (ob >= 0 && ob < (int)d.len) a |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
+          }
+          wv[b] = a;
         }
-        hist_crc[0] = acc_crc;
-        hist_vbits[0] = acc_vbits;
-        run0 = s;
-        acc_vbits = 0;
+        process_block<false>(L, d, blk, make_uint4(wv[0], wv[1], wv[2], wv[3]), ce);
       }
-    };
-    // Whole rounds of DEPTH steps with one uniform trip test, then the remainder: early exits
-    // inside the round would merge into the loop latch and the wait-count state at the loop
-    // header would include the exit paths' fresh loads (vmcnt(0) every round).
-    if (DEPTH == 2) {
-      while (s + 2 <= s_end) {
-        step(A, B);
-        step(B, A);
+      const uint32_t crc = ~group_lin(L, ce);
+      const uint32_t ok = (len >= 5u && __builtin_bswap32(ce.tr) == crc) ? 1u : 0u;
+      const uint64_t f = (uint64_t)e * 4 + (uint64_t)L.grp;
+      if (L.col == 15 && f < p.nframes) {
+        if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crc;
+        if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)ok;
+        if (SEAL) write_trailer(f, crc);
       }
-      if (s < s_end) step(A, B);
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+  }
+
+
+  Chains c{0u, 0u, 0u, 0u, 0u};
+  // One step: [read the claim issued two steps ago] [issue a claim] [prefetch] [compute +
+  // finish the current set if it exists].  Static: the sequence is contiguous.
+  auto step = [&](ItemBuf<J>& cur, ItemBuf<J>& fill, uint32_t& c_issue, uint32_t& c_read) {
+    uint32_t q_load;
+    if (DYN) {
+      q_load = claim_set(c_read);
+      c_issue = claim_issue();
     } else {
-      while (s + 3 <= s_end) {
-        step(A, C);
-        step(B, A);
-        step(C, B);
-      }
-      if (s < s_end) step(A, C);
-      if (s < s_end) step(B, A);
+      q_load = (DEPTH == 3) ? q_nx2 : q_nx1;
     }
-    // hist[r] holds run nruns-1-r; runs start every 16 sets from s_main.
-    const uint64_t nsets_main = s_end - s_main;
-    const int nruns = (int)((nsets_main + kSetsPerRun - 1) / kSetsPerRun);
-#pragma unroll
-    for (int r = 0; r < kLeanRuns; r++) {
-      const int q = nruns - 1 - r;
-      if (q >= 0) {
-        const uint64_t first = s_main + (uint64_t)q * kSetsPerRun;
-        const int cnt = (int)min((uint64_t)kSetsPerRun, s_end - first);
-        store_run(first, cnt, hist_crc[r], hist_vbits[r]);
-      }
+    if (ABL != kLeanAblCompute) load(q_load, fill);
+    // Issue the prefetch before the first wait on `cur`: a wave whose data is late must not
+    // also hold back its next requests.
+    __builtin_amdgcn_sched_barrier(0);
+    if (q_cur < q_end) {
+      compute(q_cur, cur, c);
+      finish(q_cur, c);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (DEPTH == 3) {
+      q_cur = q_nx1;
+      q_nx1 = q_load;
+      q_nx2 = q_load + 1;
+    } else {
+      q_cur = q_load;
+      q_nx1 = q_load + 1;
+    }
+  };
+  // Whole rounds of DEPTH steps with one uniform trip test (no early exits inside a round: they
+  // would merge into the loop latch and poison the wait counts at the loop header).  The claim
+  // ring rotates with period 3: step j issues into ring[j % 3] and reads ring[(j + 1) % 3].
+  if (DEPTH == 2) {
+    while (q_cur < q_end) {
+      step(A, B, cX, cY);
+      step(B, A, cY, cZ);
+      step(A, B, cZ, cX);
+      step(B, A, cX, cY);
+      step(A, B, cY, cZ);
+      step(B, A, cZ, cX);
+    }
+  } else {
+    while (q_cur < q_end) {
+      step(A, C, cX, cY);
+      step(B, A, cY, cZ);
+      step(C, B, cZ, cX);
     }
   }
+  // Results: the partial run, then the history.
+  if (t > 0) store_run((int)t, acc_crc, acc_qv);
+  store_hist();
 
-  // Edge sets [s_begin, s_main) (the first sets of the batch only): byte loads restricted to the
-  // frame, results stored per set by lane 15 of each group.
-#pragma unroll 1
-  for (uint64_t e = s_begin; e < s_main; e++) {
-    FrameDesc d = make_desc(min(e * 4 + (uint64_t)L.grp, p.nframes - 1) * stride, len);
-    Chains c{0u, 0u, 0u, 0u, 0u};
-#pragma unroll 1
-    for (int blk = 0; blk < J; blk++) {
-      uint32_t wv[4];
-#pragma unroll
-      for (int b = 0; b < 4; b++) {
-        const int o = 256 * blk + 16 * L.col + 4 * b - d.pad;
-        uint32_t a = 0;
-#pragma unroll 1
-        for (int k = 0; k < 4; k++) {
-          const int ob = o + k;
-          if (ob >= 0 && ob < (int)d.len) a |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
-        }
-        wv[b] = a;
-      }
-      process_block<false>(L, d, blk, make_uint4(wv[0], wv[1], wv[2], wv[3]), c);
-    }
-    acc_vbits = 0;
-    finish(15, c);  // lane 15 of each group receives the crc and (bit 15) the valid flag
-    const uint64_t f = e * 4 + (uint64_t)L.grp;
-    if (L.col == 15 && f < p.nframes) {
-      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = acc_crc;
-      if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)((acc_vbits >> 15) & 1u);
-      if (SEAL) write_trailer(f, acc_crc);
+  if (DYN) {  // the workgroup's last wave resets the claim counters for the next launch
+    uint32_t done = 0;
+    if (L.lane == 0) done = __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(done) == wpb - 1 && L.lane == 0) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+#ifdef UFC_TUNING
+  if (p.dbg && L.lane == 0) {
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* d = p.dbg + 4 * w;
+    d[0] = t_start;
+    d[1] = t_staged;
+    d[2] = t_end;
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+    d[3] = (unsigned long long)(q_end - q_lo) | ((unsigned long long)__smid() << 32) | ((unsigned long long)xcc << 56);
+  }
+#endif
 }
 
-#define UFC_INST_FIXED(J)                                                                \
-  template __global__ void frame_crc_fixed_kernel<J, false, 2, 0>(const KernelParams);   \
-  template __global__ void frame_crc_fixed_kernel<J, true, 2, 0>(const KernelParams);    \
-  template __global__ void frame_crc_fixed_kernel<J, false, 3, 0>(const KernelParams);   \
-  template __global__ void frame_crc_fixed_kernel<J, true, 3, 0>(const KernelParams);
+#define UFC_INST_FIXED(J)                                                                      \
+  template __global__ void frame_crc_fixed_kernel<J, false, 3, 0, true>(const KernelParams);   \
+  template __global__ void frame_crc_fixed_kernel<J, true, 3, 0, true>(const KernelParams);
 UFC_INST_FIXED(1) UFC_INST_FIXED(2) UFC_INST_FIXED(3) UFC_INST_FIXED(4) UFC_INST_FIXED(5) UFC_INST_FIXED(6)
 
 #ifdef UFC_TUNING
-template __global__ void frame_crc_fixed_kernel<6, false, 2, kLeanAblLoads>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 2, kLeanAblCompute>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute>(const KernelParams);
+// A/B variants (J = 6, validate): static schedule, depth 2, ablations.
+template __global__ void frame_crc_fixed_kernel<6, false, 3, 0, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 2, 0, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, true>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, false>(const KernelParams);
+template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, false>(const KernelParams);
 #endif
 
-const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl) {
-  if (depth != 2 && depth != 3) return nullptr;
-#define UFC_PICK_FIXED(JJ)                                                                                  \
-  if (J == JJ && abl == 0) {                                                                                \
-    if (depth == 2) return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 2, 0>                      \
-                                : (const void*)frame_crc_fixed_kernel<JJ, false, 2, 0>;                    \
-    return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0> : (const void*)frame_crc_fixed_kernel<JJ, false, 3, 0>; \
-  }
-  UFC_PICK_FIXED(1) UFC_PICK_FIXED(2) UFC_PICK_FIXED(3) UFC_PICK_FIXED(4) UFC_PICK_FIXED(5) UFC_PICK_FIXED(6)
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, bool dyn) {
+  if (abl == 0 && depth == 3 && dyn) {
+    switch (J) {
+#define UFC_PICK_FIXED(JJ) \
+  case JJ: return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0, true> : (const void*)frame_crc_fixed_kernel<JJ, false, 3, 0, true>;
+      UFC_PICK_FIXED(1) UFC_PICK_FIXED(2) UFC_PICK_FIXED(3) UFC_PICK_FIXED(4) UFC_PICK_FIXED(5) UFC_PICK_FIXED(6)
 #undef UFC_PICK_FIXED
+      default: return nullptr;
+    }
+  }
 #ifdef UFC_TUNING
   if (J == 6 && !seal) {
-    if (abl == kLeanAblLoads)
-      return depth == 2 ? (const void*)frame_crc_fixed_kernel<6, false, 2, kLeanAblLoads>
-                        : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads>;
-    if (abl == kLeanAblCompute)
-      return depth == 2 ? (const void*)frame_crc_fixed_kernel<6, false, 2, kLeanAblCompute>
-                        : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute>;
+    if (abl == 0 && depth == 3 && !dyn) return (const void*)frame_crc_fixed_kernel<6, false, 3, 0, false>;
+    if (abl == 0 && depth == 2 && dyn) return (const void*)frame_crc_fixed_kernel<6, false, 2, 0, true>;
+    if (depth == 3 && abl == kLeanAblLoads)
+      return dyn ? (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, true>
+                 : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, false>;
+    if (depth == 3 && abl == kLeanAblCompute)
+      return dyn ? (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, true>
+                 : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, false>;
   }
 #endif
   return nullptr;

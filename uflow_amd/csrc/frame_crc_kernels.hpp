@@ -26,18 +26,24 @@ struct KernelParams {
   const uint32_t* chain_tab;  // device: 1024 words (A^256 byte tables)
   const uint32_t* nib_img;    // device: 8192 words (per-slot nibble tables, LDS image order)
   uint32_t G;                 // A^-4(~0)
+  uint32_t* ctr;              // lean fixed kernel: per-workgroup claim counters (zero at launch)
+  uint32_t front_ok;          // lean fixed kernel: the pad bytes before frame 0 are readable
+  unsigned long long* dbg;    // tuning builds only: per-wave timestamps (nullptr in product use)
 };
 
 // Kernel entry for (JC 256-byte blocks per pipelined part, mode); nullptr if not instantiated.
 const void* kernel_symbol(int jc, int mode);
 bool config_available(int jc);
 // Lean fixed-length kernel (frame_len >= 4, J = ceil((frame_len + 4) / 256) in 1..6); one
-// workgroup per CU, each wave a balanced contiguous range of 4-frame sets, `depth` (2 or 3) sets
-// in flight per wave.  abl != 0 selects the ablation variants of tuning builds (J = 6 only).
+// workgroup per CU owning a contiguous range of 4-frame sets, handed to its 16 waves dynamically
+// (dyn) or as static per-wave ranges (tuning A/B); `depth` (2 or 3) sets in flight per wave.
+// abl != 0 selects the ablation variants of tuning builds (J = 6 only).
 constexpr int kLeanDepthDefault = 3;
 // Results stay in registers until a wave's range is done: at most 16 * kLeanRuns sets per wave,
 // i.e. a launch covers at most (waves in the grid) * 16 * kLeanRuns * 4 frames (host-chunked).
 constexpr int kLeanRuns = 8;
-const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl);
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, bool dyn);
+// Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
+constexpr int kCtrWordsPerBlock = 32;
 
 }  // namespace ufc_dev

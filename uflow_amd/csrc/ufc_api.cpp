@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,7 +35,14 @@ struct ufc_ctx {
   uint64_t* h_off_pinned = nullptr;
   size_t h_off_cap = 0;
   hipStream_t streams[2] = {nullptr, nullptr};
+  // Claim counters of the lean fixed kernel: kCtrSlots slots of ncu * kCtrWordsPerBlock words,
+  // zeroed at creation and reset by each launch's last wave; launches take slots round-robin, so
+  // concurrent launches on different streams do not share counters (up to kCtrSlots in flight).
+  uint32_t* d_ctr = nullptr;
+  std::atomic<uint32_t> ctr_seq{0};
 };
+
+constexpr uint32_t kCtrSlots = 64;
 
 namespace {
 
@@ -102,18 +110,23 @@ int lean_fixed_blocks(uint64_t frame_len) {
 
 int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
   int depth = ufc_dev::kLeanDepthDefault, abl = 0;
-  if (const char* d = std::getenv("UFC_LEAN_DEPTH")) depth = std::atoi(d);
+  bool dyn = true;
 #ifdef UFC_TUNING
-  if (const char* ab = std::getenv("UFC_LEAN_ABL"); ab && !seal) abl = std::atoi(ab);
+  // A/B knobs of the validate path (tuning builds): pipeline depth, schedule, ablations.
+  if (!seal) {
+    if (const char* d = std::getenv("UFC_LEAN_DEPTH")) depth = std::atoi(d);
+    if (const char* ab = std::getenv("UFC_LEAN_ABL")) abl = std::atoi(ab);
+    if (const char* dy = std::getenv("UFC_LEAN_DYN")) dyn = std::atoi(dy) != 0;
+  }
 #endif
-  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl);
+  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl, dyn);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain;
   kp.nib_img = ctx->d_nib;
   kp.G = ctx->G;
-  // One 1024-thread workgroup per CU; a wave's results stay in registers, so one launch covers
-  // at most 16 * kLeanRuns sets per wave: larger batches go in chunks (every frame in a chunk
-  // keeps its absolute address, so only the first sets of a chunk take the edge path).
+  // One 1024-thread workgroup per CU.  A launch covers at most `chunk` frames (32-bit set
+  // indices; a wave's results mostly stay in registers until the end); every frame of a chunk
+  // keeps its absolute address, and chunks after the first may read the pad bytes before them.
   const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
   const uint64_t chunk = (uint64_t)ctx->ncu * waves_per_block * 16 * ufc_dev::kLeanRuns * 4;
   const uint64_t total = kp.nframes;
@@ -124,13 +137,35 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
     if (kp.wbytes) c.wbytes = kp.wbytes + f0 * kp.stride;
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
+    c.front_ok = f0 > 0 ? 1u : 0u;
+    // Claim counters: one slot of the ring per launch (zero on entry, reset by the kernel).
+    const uint32_t slot = ctx->ctr_seq.fetch_add(1) % kCtrSlots;
+    c.ctr = ctx->d_ctr + (size_t)slot * ctx->ncu * ufc_dev::kCtrWordsPerBlock;
     const uint64_t nsets = (c.nframes + 3) / 4;
     uint64_t blocks = (nsets + waves_per_block - 1) / waves_per_block;
     if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
     if (blocks < 1) blocks = 1;
+#ifdef UFC_TUNING
+    // UFC_DBG_WAVES=<file>: per-wave timestamps of this launch (synchronous; tuning only).
+    const char* dbg_path = std::getenv("UFC_DBG_WAVES");
+    unsigned long long* d_dbg = nullptr;
+    if (dbg_path && hipMalloc(&d_dbg, blocks * waves_per_block * 32) == hipSuccess) c.dbg = d_dbg;
+#endif
     void* args[] = {&c};
     hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
+#ifdef UFC_TUNING
+    if (d_dbg) {
+      std::vector<unsigned long long> h(blocks * waves_per_block * 4);
+      (void)hipStreamSynchronize(stream);
+      (void)hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost);
+      (void)hipFree(d_dbg);
+      if (FILE* f = std::fopen(dbg_path, "wb")) {
+        std::fwrite(h.data(), 8, h.size(), f);
+        std::fclose(f);
+      }
+    }
+#endif
   }
   return UFC_OK;
 }
@@ -228,7 +263,10 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
   if ((e = hipMalloc(&ctx->d_chain, chain.size() * 4)) != hipSuccess ||
       (e = hipMalloc(&ctx->d_nib, nib.size() * 4)) != hipSuccess ||
       (e = hipMemcpy(ctx->d_chain, chain.data(), chain.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
-      (e = hipMemcpy(ctx->d_nib, nib.data(), nib.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) {
+      (e = hipMemcpy(ctx->d_nib, nib.data(), nib.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_ctr, (size_t)kCtrSlots * ctx->ncu * ufc_dev::kCtrWordsPerBlock * 4)) != hipSuccess ||
+      (e = hipMemset(ctx->d_ctr, 0, (size_t)kCtrSlots * ctx->ncu * ufc_dev::kCtrWordsPerBlock * 4)) != hipSuccess ||
+      (e = hipDeviceSynchronize()) != hipSuccess) {
     ufc_ctx_destroy(ctx);
     return UFC_ERR_HIP;
   }
@@ -243,6 +281,7 @@ int ufc_ctx_destroy(ufc_ctx* ctx) {
     DeviceGuard g(ctx->device >= 0 ? ctx->device : 0);
     if (ctx->d_chain) (void)hipFree(ctx->d_chain);
     if (ctx->d_nib) (void)hipFree(ctx->d_nib);
+    if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_off) (void)hipFree(ctx->d_off);
     if (ctx->d_crc) (void)hipFree(ctx->d_crc);
