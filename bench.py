@@ -178,7 +178,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "frame_crc_kernel<6,0> (ufc_crc_batch_fixed)",
+                "kernel": "ufc_dev::frame_crc_fixed_kernel<6,false,3,0,true> (ufc_crc_batch_fixed)",
                 "kernel_avg_ms": round(kern_ms, 4),
                 "algorithmic_bytes_per_launch": algo_bytes,
                 **({"traffic_source": tsrc} if tsrc else {}),

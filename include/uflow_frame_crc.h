@@ -27,7 +27,10 @@
  *   - Device entry points are asynchronous on `stream` (a hipStream_t, or NULL for the null
  *     stream), allocate nothing per call, and never fall back to the CPU: without a usable
  *     MI355X (gfx950) device ufc_ctx_create fails with UFC_ERR_NO_DEVICE.
- *   - One ufc_ctx per device per host thread; the scalar host functions are reentrant.
+ *   - One ufc_ctx per device.  Device launches on different streams of one context are safe while
+ *     fewer than 64 are in flight (each takes a claim-counter slot); ufc_validate_host_varlen
+ *     uses the context's own streams and staging, one host thread at a time per context.  The
+ *     scalar host functions are reentrant.
  */
 #ifndef UFLOW_FRAME_CRC_H
 #define UFLOW_FRAME_CRC_H
