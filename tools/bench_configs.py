@@ -52,12 +52,22 @@ def varlen(eng, dev, n=10_000_000, reps=20):
     torch.cuda.synchronize()
     expect = n - len(range(0, n, 997))
     ok = int(valid.sum()) == expect
+    # bit-exact check of a sample (the first 200k frames) against the CPU oracle
+    import oracle
+    k = 200_000
+    off_h = offsets[: k + 1].cpu().numpy().astype(np.uint64)
+    ref_crc, ref_valid = oracle.validate_varlen(data[: int(off_h[-1])].cpu().numpy(), off_h)
+    exact = bool(np.array_equal(crc[:k].cpu().numpy().view(np.uint32), ref_crc) and
+                 np.array_equal(valid[:k].cpu().numpy(), ref_valid))
     ms = timed(fn, reps, s)
+    os.environ["UFC_VARLEN_KERNEL"] = "generic"  # A/B: the generic kernel on the same batch
+    ms_generic = timed(fn, reps, s)
+    del os.environ["UFC_VARLEN_KERNEL"]
     algo = total + 8 * (n + 1) + 4 * n + n
     return {"config": "3: varlen 10M x U[64,1500] device-resident", "frames": n, "bytes": total,
             "kernel_ms": round(ms, 4), "GiB_s": round(total / ms / 1e-3 / 2**30, 1),
             "algo_GB_s": round(algo / ms / 1e-3 / 1e9, 1), "hbm_frac": round(algo / ms / 1e-3 / 8e12, 4),
-            "valid_ok": ok}
+            "valid_ok": ok, "sample_bit_exact": exact, "generic_kernel_ms": round(ms_generic, 4)}
 
 
 def shard(eng, dev, n=12_500_000, L=1500, reps=10):

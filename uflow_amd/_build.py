@@ -11,8 +11,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libuflowcrc.so")
-SOURCES = ["frame_crc.hip", "ufc_api.cpp", "crc_math.cpp"]
-HEADERS = ["frame_crc_kernels.hpp", "crc_math.hpp"]
+SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "ufc_api.cpp", "crc_math.cpp"]
+HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 

@@ -43,6 +43,11 @@ constexpr int kLeanDepthDefault = 3;
 // i.e. a launch covers at most (waves in the grid) * 16 * kLeanRuns * 4 frames (host-chunked).
 constexpr int kLeanRuns = 8;
 const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, bool dyn);
+// Lean variable-length kernel (CSR offsets, any frame lengths; frames of 4..1532 B on the fast
+// path, the rest byte-wise after the main loop).  Set indices are 30-bit: a launch covers fewer
+// than 2^32 frames (host-chunked).
+// abl != 0: ablation variants of tuning builds (validate only).
+const void* varlen_kernel_symbol(bool seal, int abl);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

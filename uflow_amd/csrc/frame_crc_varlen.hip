@@ -1,0 +1,424 @@
+// frame_crc_varlen.hip -- lean variable-length frame-CRC kernel for MI355X / gfx950.
+//
+// The batched CRC gate of Frame::read (src/frame/serial/mod.rs:675-690) and the frame seal
+// (src/frame/serial/mod.rs:463-470, src/frame/serial/build.rs:151-159) over a CSR batch: frame i
+// is bytes[offsets[i] .. offsets[i+1]).  This is how received datagrams arrive (uflow frames are
+// 5..1472 B, src/lib.rs:294) and BASELINE.json config 3 (10M frames of U[64,1500] B).
+//
+// Same math, LDS tables and wave layout as the fixed-length kernels (frame_crc_dev.hpp); the
+// schedule is the lean fixed kernel's with per-frame geometry:
+//   * A set is 4 consecutive frames, one per 16-lane group, so neighbouring frames' shared
+//     boundary lines are read by one wave within a few instructions.
+//   * Frame g loads exactly its J_g 256-byte blocks [start - pad, start + len).  A set always
+//     issues 6 block loads, so hipcc's wait counts stay static whatever the mix of lengths: they
+//     are raw buffer loads on a per-set resource (scalar base = the set's first frame - 512), and
+//     blocks past J_g get an out-of-range offset, which returns zeros without a memory request.
+//     (Re-reading a block instead costs its full bytes again: non-temporal lines are not kept.)
+//   * Loads are 4-byte aligned: a frame's window [start - pad, start + len) starts anywhere, and a
+//     misaligned dwordx4 costs the load path ~15 % (measured).  The window is loaded from its
+//     start rounded up to 4 bytes (dl = 0..3 bytes later) and each word is rebuilt with one
+//     v_perm_b32 from the loaded word and its predecessor: the lane's previous word, the previous
+//     lane's last word (DPP row_ror:1), or for lane 0 the previous block's lane-15 word.  The
+//     window's first dl bytes are pad (synthesised anyway); its last dl loaded bytes lie past the
+//     frame, so frames ending within 3 bytes of the batch end take the byte path.
+//   * The set computes max_g J_g blocks (a uniform branch per block); frame g freezes its chains
+//     after block J_g - 1, whose lane-15 last word is its trailer.
+//   * Offsets: lane (g, col) loads offsets[4q + g + (col & 1)] (one dwordx2) and swaps with its
+//     quad neighbour (DPP), so every lane holds its frame's [start, end).  Scalar loads would be
+//     one instruction per set, but they share lgkmcnt with LDS, so every table lookup of the
+//     compute would wait for them.  Per step k: read the claim for set k+4, issue the next claim,
+//     issue set k+4's offsets, turn set k+2's offsets (issued in step k-2, before set k's data,
+//     so this wait never covers set k's data) into its geometry, issue its 6 block loads,
+//     compute set k.
+//   * Results leave once per run of 16 sets through global stores written as inline asm.  hipcc
+//     never sees them, so its wait-count model keeps counting loads only; a store it could see
+//     would make every later load wait vmcnt(0), since loads and stores share vmcnt and may
+//     complete out of order.  Hidden stores can only make a counted wait stricter (loads return
+//     in order), never looser.
+//   * Sets the fast path cannot take -- a frame shorter than 4 B or longer than 6 blocks, pad
+//     bytes before the buffer, the partial last set -- run byte-wise in the loop (rare: the loads
+//     and waits of that branch only drain this wave's pipeline).
+#include "frame_crc_dev.hpp"
+
+namespace ufc_dev {
+
+__device__ __forceinline__ void st_u32_hidden(uint32_t* a, uint32_t v) {
+  asm volatile("global_store_dword %0, %1, off" : : "v"(a), "v"(v));
+}
+__device__ __forceinline__ void st_u8_hidden(uint8_t* a, uint32_t v) {
+  asm volatile("global_store_byte %0, %1, off" : : "v"(a), "v"(v));
+}
+
+// Per-lane pick between two uniform values by a constant lane mask (v_cndmask_b32).  Written as
+// asm: hipcc turns a select chain over the lane's group into an indexed scratch-memory table.
+__device__ __forceinline__ uint32_t lane_pick32(uint64_t mask, uint32_t t, uint32_t f) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(mask));
+  return r;
+}
+__device__ __forceinline__ uint64_t lane_pick64(uint64_t mask, uint64_t t, uint64_t f) {
+  return (uint64_t)lane_pick32(mask, (uint32_t)t, (uint32_t)f) |
+         ((uint64_t)lane_pick32(mask, (uint32_t)(t >> 32), (uint32_t)(f >> 32)) << 32);
+}
+constexpr uint64_t kOddLanes = 0xAAAAAAAAAAAAAAAAull;
+
+// Packed per-lane geometry of one set: pad (bits 0..8), J (bits 9..12), len >= 5 (bit 13),
+// realignment dl (bits 14..15).
+__device__ __forceinline__ int vl_pad(uint32_t g) { return (int)(g & 511u); }
+__device__ __forceinline__ int vl_J(uint32_t g) { return (int)((g >> 9) & 15u); }
+// v_perm_b32 selector taking the 4 bytes that start dl bytes before word `hi` of {hi, lo}.
+__device__ __forceinline__ uint32_t vl_sel(uint32_t g) { return 0x03020100u + (4u - ((g >> 14) & 3u)) * 0x01010101u; }
+
+// Front fix of a word of block 0 (or word 0 of block 1): d = bytes of the word that precede the
+// frame.  Bytes at frame offsets [-4, 0) are G's, below -4 zeros: x' = (x & dm) | pre.
+__device__ __forceinline__ uint32_t vl_fix(uint32_t x, int d, uint32_t G) {
+  const uint32_t dm = d <= 0 ? 0xFFFFFFFFu : (d < 4 ? (0xFFFFFFFFu << (8 * d)) : 0u);
+  const uint32_t pre = (d > 0 && d < 8) ? (uint32_t)(((uint64_t)G << 32) >> ((64 - 8 * d) & 63)) : 0u;
+  return __builtin_amdgcn_bitop3_b32(x, dm, pre, 0xEA);  // (x & dm) | pre
+}
+
+struct SetMeta {   // uniform part of a set's geometry
+  int Jset;        // max_g J_g
+  bool slow;       // byte path
+};
+
+constexpr int kVlBlocks = 6;      // fast-path blocks per frame (frames of 4..1532 B)
+constexpr uint32_t kVlBias = 512;  // lane offsets are relative to (start of frame 0) - 512
+// Raw buffer resource of a set: num_records far above any fast-path offset (< 2^20 + 2^11);
+// kVlOob is out of range (the load returns zeros and makes no memory request).
+constexpr uint32_t kVlRecords = 0x7FFFFFF0u;
+constexpr uint32_t kVlOob = 0x80000000u;
+constexpr int kRsrcWord3 = 0x00020000;  // gfx9-family raw buffer descriptor word 3
+constexpr int kAuxNT = 2;               // cache policy bits of the load: nt (streaming)
+
+// ABL (tuning builds only; results meaningless): bit 0 = loads + XOR fold, no CRC; bit 1 = CRC
+// of register data, no block loads (offsets and geometry kept); bit 2 = global loads instead of
+// buffer loads (unused blocks re-read block 0; sets that are not live read the nibble image).
+template <bool SEAL, int ABL>
+__global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  const StageRegs sr = stage_load(p);
+  Lane L;
+  init_lane(L, lds, p.G);
+  constexpr int JM = kVlBlocks;
+  const uint64_t nfr = p.nframes;
+  const uint32_t nsets = (uint32_t)((nfr + 3) >> 2);  // < 2^30 (host chunks launches)
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t q_lo = (uint32_t)((uint64_t)nsets * blockIdx.x / gridDim.x);
+  const uint32_t q_end = (uint32_t)((uint64_t)nsets * (blockIdx.x + 1) / gridDim.x);
+  uint32_t* ctr = p.ctr + blockIdx.x * kCtrWordsPerBlock;
+  auto claim_issue = [&]() -> uint32_t {
+    uint32_t v = 0;
+    if (L.lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  };
+  // Sets 0..3 of each wave are static (lo + 16i + wid); the rest are claimed.
+  auto claim_set = [&](uint32_t v) -> uint32_t { return q_lo + 4 * wpb + __builtin_amdgcn_readfirstlane(v); };
+  // offsets[4q + g + (col & 1)] (clamped): even lanes get the frame's start, odd lanes its end.
+  auto load_off = [&](uint32_t q) -> uint64_t {
+    const uint64_t i = 4 * (uint64_t)min(q, nsets - 1) + (uint64_t)L.grp + (uint64_t)(L.col & 1);
+    return *as_global<g_u64>(p.offsets + (i < nfr ? i : nfr));
+  };
+  const uint32_t lane16 = 16u * (uint32_t)L.col;
+  const uint64_t buf_end = *as_global<g_u64>(p.offsets + nfr);  // end of the batch's bytes
+
+  // Geometry of set q from its offsets: lane offset of block 0 (voff0), packed per-lane geometry,
+  // the set's scalar base and uniform meta.  A set that is not live (past the range, or slow)
+  // loads nothing (voff0 out of range).
+  auto geometry = [&](uint32_t q, uint64_t mine, const uint8_t*& sbase, uint32_t& voff0, SetMeta& m) -> uint32_t {
+    const uint32_t lo = (uint32_t)mine, hi = (uint32_t)(mine >> 32);
+    const uint32_t plo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+    const uint32_t phi = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0xB1, 0xF, 0xF, false);
+    const uint64_t other = (uint64_t)plo | ((uint64_t)phi << 32);
+    const uint64_t a = lane_pick64(kOddLanes, other, mine), b = lane_pick64(kOddLanes, mine, other);
+    const uint64_t a0 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, 0) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), 0) << 32);
+    const uint64_t len = b - a, rel = a - a0;
+    const uint32_t l32 = (uint32_t)min(len, (uint64_t)0x40000000u);
+    const uint32_t n = l32 >= 4u ? l32 - 4u : l32;
+    const uint32_t J = min((n + 8u + 255u) >> 8, 15u);
+    const uint32_t pad = (J * 256u - (n + 4u)) & 511u;
+    const uint32_t dl = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - pad)) & 3u;
+    const bool bad = l32 < 4u || J > (uint32_t)JM || a < (uint64_t)pad || rel > (1u << 20) || b + 3 > buf_end;
+    m.slow = __builtin_amdgcn_ballot_w64(bad) != 0;
+    m.Jset = max(max(__builtin_amdgcn_readlane((int)J, 0), __builtin_amdgcn_readlane((int)J, 16)),
+                 max(__builtin_amdgcn_readlane((int)J, 32), __builtin_amdgcn_readlane((int)J, 48)));
+    const bool live = q < q_end && !m.slow;
+    sbase = p.bytes + a0 - kVlBias;
+    voff0 = live ? (uint32_t)rel + kVlBias - pad + dl + lane16 : kVlOob;
+    return pad | (J << 9) | ((l32 >= 5u ? 1u : 0u) << 13) | (dl << 14);
+  };
+  // The 6 block loads of a set: blocks past the frame's J (and every block of a set that is not
+  // live) are out of range.
+  auto load_set6 = [&](const uint8_t* sbase, uint32_t voff0, uint32_t geo, ItemBuf<JM>& buf) {
+    const int J = vl_J(geo);
+    if (ABL & 4) {
+      const bool live = voff0 != kVlOob;
+      const uint8_t* gb = live ? sbase : (const uint8_t*)p.nib_img;
+      const uint32_t v0 = live ? voff0 : lane16;
+#pragma unroll
+      for (int j = 0; j < JM; j++) {
+        const uint32_t vo = (j < J) ? v0 + 256u * j : v0;
+        const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(gb + vo));
+        buf.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+      return;
+    }
+    if (ABL & 2) {  // register data derived from the geometry instead of loads
+#pragma unroll
+      for (int j = 0; j < JM; j++) buf.x[j] = make_uint4(voff0 + j, geo, voff0 ^ geo, (uint32_t)j * J);
+      return;
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sbase, 0, (int)kVlRecords, kRsrcWord3);
+    // Cache policy (tuning A/B, bits 3/4 of ABL): block 0 carries the pad, i.e. the previous
+    // frame's tail, which that frame's last block reads again.
+    constexpr int kAux0 = (ABL & 8) ? 0 : kAuxNT;
+    constexpr int kAuxN = (ABL & 16) ? 0 : kAuxNT;
+    {
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff0, 0, kAux0);
+      buf.x[0] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+#pragma unroll
+    for (int j = 1; j < JM; j++) {
+      const uint32_t vo = (j < J) ? voff0 + 256u * j : kVlOob;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kAuxN);
+      buf.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+
+  // ---- results: lane (g, col = t) holds frame g of the run's t-th set; qv = q | slow << 30 |
+  // valid << 31.  A full run leaves through hidden stores. ----
+  uint32_t acc_crc = 0, acc_qv = 0;
+  uint32_t t = 0;  // sets in the current run (uniform)
+  auto store_run = [&](int cnt) {
+    const uint64_t f = (uint64_t)(acc_qv & 0x3FFFFFFFu) * 4 + (uint64_t)L.grp;
+    if (L.col < cnt && f < nfr && !(acc_qv & 0x40000000u)) {
+      if (p.crc_out) st_u32_hidden(p.crc_out + f, acc_crc);
+      if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_qv >> 31);
+    }
+  };
+  auto record = [&](uint32_t crc, uint32_t qv) {
+    acc_crc = (L.col == (int)t) ? crc : acc_crc;
+    acc_qv = (L.col == (int)t) ? qv : acc_qv;
+    if (++t == kSetsPerRun) {
+      store_run(kSetsPerRun);
+      t = 0;
+    }
+  };
+  // Seal: lanes 12..15 of each group write the BE32 CRC into the frame's last 4 bytes (hidden
+  // byte stores; the frame's trailer address = sbase + voff0 - dl - 16 col + 256 J - 4).
+  auto seal_trailer = [&](const uint8_t* sbase, uint32_t voff0, uint32_t geo, uint32_t crc) {
+    if (L.col >= 12) {
+      const uint32_t k = (uint32_t)L.col - 12u;
+      const uint32_t dl = (geo >> 14) & 3u;
+      uint8_t* a = (uint8_t*)p.wbytes + (sbase - p.bytes) + (voff0 - dl - lane16 + 256u * (uint32_t)vl_J(geo) - 4u + k);
+      st_u8_hidden(a, crc >> (24 - 8 * k));
+    }
+  };
+
+  // Fast set: Jset blocks, frame g frozen after its own J_g.
+  auto compute = [&](uint32_t geo, int Jset, const ItemBuf<JM>& b) -> uint2 {
+    if (ABL & 1) {
+      uint32_t f = geo;
+#pragma unroll
+      for (int j = 0; j < JM; j++) f ^= b.x[j].x ^ b.x[j].y ^ b.x[j].z ^ b.x[j].w;
+      return make_uint2(f, f & 1u);
+    }
+    const int J = vl_J(geo);
+    const int d0 = vl_pad(geo) - 16 * L.col;
+    const uint32_t sel = vl_sel(geo);
+    // Realigned block j: words rebuilt from the loaded words (see the header comment); rp = the
+    // previous lane's last loaded word of block j - 1 (row_ror:1), for lane 0.
+    uint32_t rp = 0;
+    auto realign = [&](const uint4& w) -> uint4 {
+      const uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)w.w, 0x121, 0xF, 0xF, false);  // row_ror:1
+      const uint32_t prev = (L.col == 0) ? rp : r;
+      rp = r;
+      return make_uint4(perm(w.x, prev, sel), perm(w.y, w.x, sel), perm(w.z, w.y, sel), perm(w.w, w.z, sel));
+    };
+    Chains c;
+    {
+      uint4 x = realign(b.x[0]);
+      const bool last = (J == 1);
+      c.tr = x.w;
+      x.w = (last && L.col == 15) ? 0u : x.w;
+      c.v0 = vl_fix(x.x, d0, L.G);
+      c.v1 = vl_fix(x.y, d0 - 4, L.G);
+      c.v2 = vl_fix(x.z, d0 - 8, L.G);
+      c.v3 = vl_fix(x.w, d0 - 12, L.G);
+    }
+#pragma unroll
+    for (int j = 1; j < JM; j++) {
+      if (j < Jset) {
+        uint4 x = realign(b.x[j]);
+        const bool last = (j == J - 1);
+        c.tr = last ? x.w : c.tr;
+        x.w = (last && L.col == 15) ? 0u : x.w;
+        if (j == 1) x.x = vl_fix(x.x, d0 - 256, L.G);
+        const uint32_t n0 = chain_step(L.lds, c.v0, L.K, x.x);
+        const uint32_t n1 = chain_step(L.lds, c.v1, L.K, x.y);
+        const uint32_t n2 = chain_step(L.lds, c.v2, L.K, x.z);
+        const uint32_t n3 = chain_step(L.lds, c.v3, L.K, x.w);
+        const bool act = j < J;
+        c.v0 = act ? n0 : c.v0;
+        c.v1 = act ? n1 : c.v1;
+        c.v2 = act ? n2 : c.v2;
+        c.v3 = act ? n3 : c.v3;
+      }
+    }
+    const uint32_t crc = ~group_lin(L, c);
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
+    const uint32_t ok = (((geo >> 13) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
+    return make_uint2(crc, ok);
+  };
+
+  // Byte path for set q: loads restricted to each frame, any length; results stored at once,
+  // followed by vmcnt(0) so that no visible store stays pending.
+  auto slow_set = [&](uint32_t q) {
+    const uint64_t fr = 4 * (uint64_t)q + (uint64_t)L.grp;
+    const uint64_t f = fr < nfr ? fr : nfr - 1;
+    const uint64_t a = p.offsets[f], b = p.offsets[f + 1];
+    const FrameDesc d = make_desc(a, b - a);
+    const int nb = max(max(__builtin_amdgcn_readlane(d.J, 0), __builtin_amdgcn_readlane(d.J, 16)),
+                       max(__builtin_amdgcn_readlane(d.J, 32), __builtin_amdgcn_readlane(d.J, 48)));
+    Chains ce{0u, 0u, 0u, 0u, 0u};
+#pragma unroll 1
+    for (int blk = 0; blk < nb; blk++) {
+      const int bl = min(blk, d.J - 1);
+      uint32_t wv[4];
+#pragma unroll
+      for (int bb = 0; bb < 4; bb++) {
+        const int o = 256 * bl + 16 * L.col + 4 * bb - d.pad;
+        uint32_t v = 0;
+#pragma unroll 1
+        for (int k = 0; k < 4; k++) {
+          const int ob = o + k;
+          if (ob >= 0 && ob < (int)d.len) v |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
+        }
+        wv[bb] = v;
+      }
+      process_block<true>(L, d, blk, make_uint4(wv[0], wv[1], wv[2], wv[3]), ce);
+    }
+    const uint32_t crc = ~group_lin(L, ce);
+    const uint32_t ok = (d.len >= 5u && __builtin_bswap32(ce.tr) == crc) ? 1u : 0u;
+    if (L.col == 15 && fr < nfr) {
+      if (p.crc_out) *as_global<g_u32w>(p.crc_out + fr) = crc;
+      if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + fr) = (uint8_t)ok;
+      if (SEAL && d.len >= 4u) {
+        g_u8w* w = as_global<g_u8w>(p.wbytes + d.start + d.n);
+        w[0] = (uint8_t)(crc >> 24);
+        w[1] = (uint8_t)(crc >> 16);
+        w[2] = (uint8_t)(crc >> 8);
+        w[3] = (uint8_t)crc;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+  };
+
+  // ---- prologue: static sets 0..3, claims for sets 4 and 5, data of sets 0 and 1 ----
+  uint32_t S0 = q_lo + wid, S1 = q_lo + wpb + wid, S2 = q_lo + 2 * wpb + wid, S3 = q_lo + 3 * wpb + wid, S4 = 0;
+  uint32_t cX = 0, cY = 0, cZ = 0;
+  cY = claim_issue();  // read in step 0 -> set 4
+  cZ = claim_issue();  // read in step 1 -> set 5
+  ItemBuf<JM> A, B, C;          // data ring: set m in slot m % 3
+  uint64_t O0, O1, O2;          // offsets ring: set m in slot m % 3
+  uint32_t g0, g1, g2;          // per-lane geometry ring
+  SetMeta m0, m1, m2;           // uniform meta ring
+  uint32_t v0 = 0, v1 = 0, v2 = 0;                               // seal: voff0 ring
+  const uint8_t *b0 = p.bytes, *b1 = p.bytes, *b2 = p.bytes;  // seal: scalar base ring
+  {
+    const uint64_t o0 = load_off(S0), o1 = load_off(S1);
+    O2 = load_off(S2);
+    O0 = load_off(S3);
+    uint32_t vo;
+    const uint8_t* sb;
+    g0 = geometry(S0, o0, sb, vo, m0);
+    load_set6(sb, vo, g0, A);
+    if (SEAL) { b0 = sb; v0 = vo; }
+    g1 = geometry(S1, o1, sb, vo, m1);
+    load_set6(sb, vo, g1, B);
+    if (SEAL) { b1 = sb; v1 = vo; }
+  }
+  stage_store(sr, lds);
+
+  // One step (see the header comment).  cur/gc/mc: set S0; ro/fill/gf/mf: set S2; wo: set S4.
+  auto step = [&](ItemBuf<JM>& cur, uint32_t& gc, SetMeta& mc, const uint8_t*& bc, uint32_t& vc, uint64_t& ro,
+                  uint64_t& wo, ItemBuf<JM>& fill, uint32_t& gf, SetMeta& mf, const uint8_t*& bf, uint32_t& vf,
+                  uint32_t& c_issue, uint32_t& c_read) {
+    S4 = claim_set(c_read);
+    c_issue = claim_issue();
+    wo = load_off(S4);
+    {
+      const uint8_t* sb;
+      uint32_t vo;
+      gf = geometry(S2, ro, sb, vo, mf);
+      load_set6(sb, vo, gf, fill);
+      if (SEAL) { bf = sb; vf = vo; }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (S0 < q_end) {
+      if (!mc.slow) {
+        const uint2 r = compute(gc, mc.Jset, cur);
+        if (SEAL) seal_trailer(bc, vc, gc, r.x);
+        record(r.x, S0 | (r.y << 31));
+      } else {
+        slow_set(S0);
+        record(0u, S0 | 0x40000000u);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    S0 = S1;
+    S1 = S2;
+    S2 = S3;
+    S3 = S4;
+  };
+  // O(S_m) sits in slot m % 3: step k reads slot (k+2) % 3 and writes slot (k+4) % 3.
+  while (S0 < q_end) {
+    step(A, g0, m0, b0, v0, O2, O1, C, g2, m2, b2, v2, cX, cY);
+    step(B, g1, m1, b1, v1, O0, O2, A, g0, m0, b0, v0, cY, cZ);
+    step(C, g2, m2, b2, v2, O1, O0, B, g1, m1, b1, v1, cZ, cX);
+  }
+  if (t > 0) store_run((int)t);
+
+  {  // the workgroup's last wave resets the claim counters for the next launch
+    // Every claim of this wave has returned (so has been performed) before `done` is counted.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+    uint32_t done = 0;
+    if (L.lane == 0) done = __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(done) == wpb - 1 && L.lane == 0) {
+      __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+template __global__ void frame_crc_varlen_kernel<false, 0>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<true, 0>(const KernelParams);
+#ifdef UFC_TUNING
+template __global__ void frame_crc_varlen_kernel<false, 1>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, 2>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, 4>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, 5>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, 8>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, 9>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, 24>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, 25>(const KernelParams);
+#endif
+
+const void* varlen_kernel_symbol(bool seal, int abl) {
+#ifdef UFC_TUNING
+  if (!seal && abl == 1) return (const void*)frame_crc_varlen_kernel<false, 1>;
+  if (!seal && abl == 2) return (const void*)frame_crc_varlen_kernel<false, 2>;
+  if (!seal && abl == 4) return (const void*)frame_crc_varlen_kernel<false, 4>;
+  if (!seal && abl == 5) return (const void*)frame_crc_varlen_kernel<false, 5>;
+  if (!seal && abl == 8) return (const void*)frame_crc_varlen_kernel<false, 8>;
+  if (!seal && abl == 9) return (const void*)frame_crc_varlen_kernel<false, 9>;
+  if (!seal && abl == 24) return (const void*)frame_crc_varlen_kernel<false, 24>;
+  if (!seal && abl == 25) return (const void*)frame_crc_varlen_kernel<false, 25>;
+#endif
+  if (abl != 0) return nullptr;
+  return seal ? (const void*)frame_crc_varlen_kernel<true, 0> : (const void*)frame_crc_varlen_kernel<false, 0>;
+}
+
+}  // namespace ufc_dev

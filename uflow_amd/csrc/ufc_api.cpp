@@ -170,6 +170,46 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
   return UFC_OK;
 }
 
+// Lean variable-length kernel unless UFC_VARLEN_KERNEL=generic (A/B measurement).
+bool lean_varlen() {
+  const char* k = std::getenv("UFC_VARLEN_KERNEL");
+  return !(k && std::strcmp(k, "generic") == 0);
+}
+
+int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  int abl = 0;
+#ifdef UFC_TUNING
+  if (const char* ab = std::getenv("UFC_VL_ABL")) abl = std::atoi(ab);
+#endif
+  const void* fn = ufc_dev::varlen_kernel_symbol(seal, abl);
+  if (!fn) return UFC_ERR_INVALID_ARG;
+  kp.chain_tab = ctx->d_chain;
+  kp.nib_img = ctx->d_nib;
+  kp.G = ctx->G;
+  // Offsets stay absolute (relative to kp.bytes) in every chunk; a chunk only shifts the offsets
+  // and output pointers.  Chunks keep set indices below 2^30.
+  const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
+  const uint64_t chunk = (uint64_t)1 << 31;
+  const uint64_t total = kp.nframes;
+  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
+    ufc_dev::KernelParams c = kp;
+    c.nframes = std::min(chunk, total - f0);
+    c.offsets = kp.offsets + f0;
+    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
+    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
+    const uint32_t slot = ctx->ctr_seq.fetch_add(1) % kCtrSlots;
+    c.ctr = ctx->d_ctr + (size_t)slot * ctx->ncu * ufc_dev::kCtrWordsPerBlock;
+    const uint64_t nsets = (c.nframes + 3) / 4;
+    uint64_t blocks = (nsets + waves_per_block * 4 - 1) / (waves_per_block * 4);
+    if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
+    if (blocks < 1) blocks = 1;
+    void* args[] = {&c};
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+  }
+  return UFC_OK;
+}
+
 // Kernel configuration and mode bits for a fixed frame length: J = 256-byte blocks per frame.
 Config fixed_config(uint64_t frame_len, int* freeze) {
   const uint64_t n = frame_len >= 4 ? frame_len - 4 : frame_len;
@@ -333,6 +373,7 @@ int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
+  if (lean_varlen()) return launch_lean_varlen(ctx, false, kp, (hipStream_t)stream);
   return launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, (hipStream_t)stream);
 }
 
@@ -367,6 +408,7 @@ int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offs
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
+  if (lean_varlen()) return launch_lean_varlen(ctx, true, kp, (hipStream_t)stream);
   return launch(ctx, varlen_config(), ufc_dev::kModeVarlen | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
 
@@ -452,7 +494,7 @@ int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_
     kp.nframes = nf;
     kp.crc_out = dcrc;
     kp.valid_out = dval;
-    int rc = launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, s);
+    int rc = lean_varlen() ? launch_lean_varlen(ctx, false, kp, s) : launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, s);
     if (rc != UFC_OK) return rc;
     if (h_crc_out && (e = hipMemcpyAsync(h_crc_out + a, dcrc, nf * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
       return hip_fail(ctx, e);
