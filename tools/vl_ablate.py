@@ -35,7 +35,6 @@ def main():
     fn = lambda: eng.crc_varlen(data, offsets, crc_out=crc, valid_out=valid)  # noqa: E731
     out = {"frames": n, "bytes": total, "lens": [lo, hi - 1], "align": align}
     for name, env in (("full", {}), ("loads_only", {"UFC_VL_ABL": "1"}), ("compute_only", {"UFC_VL_ABL": "2"}),
-                      
                       ("generic", {"UFC_VARLEN_KERNEL": "generic"}), ("full2", {})):
         os.environ.update(env)
         fn()

@@ -91,9 +91,8 @@ constexpr uint32_t kVlOob = 0x80000000u;
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9-family raw buffer descriptor word 3
 constexpr int kAuxNT = 2;               // cache policy bits of the load: nt (streaming)
 
-// ABL (tuning builds only; results meaningless): bit 0 = loads + XOR fold, no CRC; bit 1 = CRC
-// of register data, no block loads (offsets and geometry kept); bit 2 = global loads instead of
-// buffer loads (unused blocks re-read block 0; sets that are not live read the nibble image).
+// ABL (tuning builds only; results meaningless): bit 0 = loads + XOR fold, no CRC; bit 1 = CRC of
+// register data, no block loads (offsets and geometry kept).
 template <bool SEAL, int ABL>
 __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelParams p) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
@@ -153,36 +152,24 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   // live) are out of range.
   auto load_set6 = [&](const uint8_t* sbase, uint32_t voff0, uint32_t geo, ItemBuf<JM>& buf) {
     const int J = vl_J(geo);
-    if (ABL & 4) {
-      const bool live = voff0 != kVlOob;
-      const uint8_t* gb = live ? sbase : (const uint8_t*)p.nib_img;
-      const uint32_t v0 = live ? voff0 : lane16;
-#pragma unroll
-      for (int j = 0; j < JM; j++) {
-        const uint32_t vo = (j < J) ? v0 + 256u * j : v0;
-        const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(gb + vo));
-        buf.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-      }
-      return;
-    }
     if (ABL & 2) {  // register data derived from the geometry instead of loads
 #pragma unroll
       for (int j = 0; j < JM; j++) buf.x[j] = make_uint4(voff0 + j, geo, voff0 ^ geo, (uint32_t)j * J);
       return;
     }
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sbase, 0, (int)kVlRecords, kRsrcWord3);
-    // Cache policy (tuning A/B, bits 3/4 of ABL): block 0 carries the pad, i.e. the previous
-    // frame's tail, which that frame's last block reads again.
-    constexpr int kAux0 = (ABL & 8) ? 0 : kAuxNT;
-    constexpr int kAuxN = (ABL & 16) ? 0 : kAuxNT;
     {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff0, 0, kAux0);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff0, 0, kAuxNT);
       buf.x[0] = make_uint4(v.x, v.y, v.z, v.w);
     }
+    // Every slot issues its 16-byte load, used or not: a uniform branch around a load makes
+    // hipcc's wait counts assume it may be missing (and it then turned the stand-in 4-byte loads
+    // tried here into dependent loads behind vmcnt(0)).  Each wave-level load costs the CU ~28
+    // cycles of issue even when every lane is out of range (measured).
 #pragma unroll
     for (int j = 1; j < JM; j++) {
       const uint32_t vo = (j < J) ? voff0 + 256u * j : kVlOob;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kAuxN);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kAuxNT);
       buf.x[j] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
@@ -398,24 +385,12 @@ template __global__ void frame_crc_varlen_kernel<true, 0>(const KernelParams);
 #ifdef UFC_TUNING
 template __global__ void frame_crc_varlen_kernel<false, 1>(const KernelParams);
 template __global__ void frame_crc_varlen_kernel<false, 2>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, 4>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, 5>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, 8>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, 9>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, 24>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, 25>(const KernelParams);
 #endif
 
 const void* varlen_kernel_symbol(bool seal, int abl) {
 #ifdef UFC_TUNING
   if (!seal && abl == 1) return (const void*)frame_crc_varlen_kernel<false, 1>;
   if (!seal && abl == 2) return (const void*)frame_crc_varlen_kernel<false, 2>;
-  if (!seal && abl == 4) return (const void*)frame_crc_varlen_kernel<false, 4>;
-  if (!seal && abl == 5) return (const void*)frame_crc_varlen_kernel<false, 5>;
-  if (!seal && abl == 8) return (const void*)frame_crc_varlen_kernel<false, 8>;
-  if (!seal && abl == 9) return (const void*)frame_crc_varlen_kernel<false, 9>;
-  if (!seal && abl == 24) return (const void*)frame_crc_varlen_kernel<false, 24>;
-  if (!seal && abl == 25) return (const void*)frame_crc_varlen_kernel<false, 25>;
 #endif
   if (abl != 0) return nullptr;
   return seal ? (const void*)frame_crc_varlen_kernel<true, 0> : (const void*)frame_crc_varlen_kernel<false, 0>;
