@@ -222,3 +222,78 @@ def test_varlen_misaligned_base(engine, shift):
     torch.cuda.synchronize()
     assert np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc)
     assert np.array_equal(valid.cpu().numpy(), ref_valid)
+
+
+# ---- batched Frame::read past the CRC gate (frame_parse.hip) ----
+
+def _codec_batch(rng_seed, n):
+    import random
+    from oracle import codec as C
+    rng = random.Random(rng_seed)
+    frames = []
+    for i in range(n):
+        r = i % 6
+        if r == 0:
+            frames.append(C.frame_write(C.random_data_frame(rng)))
+        elif r == 1:
+            frames.append(C.frame_write(C.random_ack_frame(rng, 30)))
+        elif r == 2:
+            frames.append(C.frame_write(C.random_sync_frame(rng)))
+        elif r == 3:
+            fb = bytearray(C.frame_write(C.random_data_frame(rng, 8)))
+            fb[rng.randrange(len(fb))] ^= 1 << rng.randrange(8)
+            frames.append(bytes(fb))
+        elif r == 4:
+            fb = bytearray(C.frame_write(C.random_data_frame(rng, 6)))
+            fb[rng.randrange(min(len(fb) - 4, 30))] = rng.getrandbits(8)  # damaged header, resealed
+            fb[-4:] = oracle.compute(bytes(fb[:-4])).to_bytes(4, "big")
+            frames.append(bytes(fb))
+        else:
+            name, fr = C.reference_test_frames()[i % 12]
+            frames.append(C.frame_write(fr))
+    offsets = np.zeros(n + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum([len(f) for f in frames])
+    return frames, np.frombuffer(b"".join(frames), dtype=np.uint8).copy(), offsets
+
+
+def test_parse_varlen_vs_oracle(engine):
+    """GPU gate + GPU parse vs the Python codec oracle, frame by frame."""
+    from oracle import codec as C
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE
+    from test_codec_cpu import info_to_dict
+    frames, data, offsets = _codec_batch(9, 3000)
+    d = torch.from_numpy(data).to(DEV)
+    o = torch.from_numpy(offsets).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    infos = infos.cpu().numpy().view(FRAME_INFO_DTYPE).reshape(-1)
+    items = items.cpu().numpy().view(ITEM_DTYPE).reshape(-1)
+    total = 0
+    for i, fb in enumerate(frames):
+        cnt = int(infos[i]["item_count"]) if infos[i]["ok"] else 0
+        assert int(infos[i]["item_first"]) == total
+        assert info_to_dict(infos[i], items[total:total + cnt], fb) == C.frame_read(fb), i
+        total += cnt
+    assert int(used.cpu()[0]) == total
+
+
+def test_parse_varlen_vs_host_parse_large(engine):
+    """A 200k-frame batch: device parse == host parse (itself pinned to the oracle on CPU)."""
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host
+    frames, data, offsets = _codec_batch(10, 600)
+    reps = 340
+    big = np.tile(data, reps)
+    lens = np.diff(offsets)
+    offs = np.zeros(len(lens) * reps + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(np.tile(lens, reps))
+    d = torch.from_numpy(big).to(DEV)
+    o = torch.from_numpy(offs).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    ref_infos, ref_items = parse_batch_host(big, offs.astype(np.uint64), valid.cpu().numpy(), nthreads=8)
+    assert np.array_equal(infos.cpu().numpy().view(FRAME_INFO_DTYPE).reshape(-1), ref_infos)
+    k = int(used.cpu()[0])
+    assert k == ref_items.size
+    assert np.array_equal(items[:k].cpu().numpy().view(ITEM_DTYPE).reshape(-1), ref_items)

@@ -20,8 +20,10 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
 def header_symbols():
-    with open(HEADER) as f:
-        text = f.read()
+    text = ""
+    for h in (HEADER, os.path.join(REPO, "include", "uflow_frame_codec.h")):
+        with open(h) as f:
+            text += f.read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(ufc_[a-z0-9_]+)\s*\(", text)))
 

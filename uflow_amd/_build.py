@@ -11,8 +11,9 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libuflowcrc.so")
-SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "ufc_api.cpp", "crc_math.cpp"]
-HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp"]
+SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_parse.hip", "ufc_api.cpp", "crc_math.cpp",
+           "frame_codec.cpp"]
+HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp", "frame_codec_core.hpp", "frame_parse.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -27,7 +28,7 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
     """tuning=True adds the ablation kernels (-DUFC_TUNING); `defines` adds -D flags (tuning
     experiments).  Both are meant with `out` pointing away from the product library."""
     deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    deps.append(os.path.join(REPO_DIR, "include", "uflow_frame_crc.h"))
+    deps += [os.path.join(REPO_DIR, "include", h) for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
     target = out or LIB_PATH
     if not force and not _stale(target, deps):
         return target

@@ -1,4 +1,5 @@
-"""ctypes binding of libuflowcrc.so (the C ABI in include/uflow_frame_crc.h).
+"""ctypes binding of libuflowcrc.so (the C ABI in include/uflow_frame_crc.h and
+include/uflow_frame_codec.h).
 
 This is the Python-side equivalent of the `extern "C"` block a Rust caller would declare
 (see INTEGRATION.md).  Loading fails loudly when the in-tree library is missing: there is no
@@ -40,8 +41,52 @@ _SIGNATURES = {
                                              ctypes.c_void_p, ctypes.c_void_p]),
     "ufc_validate_host_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                                 ctypes.c_void_p, ctypes.c_void_p]),
+    # include/uflow_frame_codec.h
+    "ufc_frame_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_size_t]),
+    "ufc_frame_write_fixed": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]),
+    "ufc_data_frame_builder_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                                   ctypes.c_int]),
+    "ufc_data_frame_builder_add": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "ufc_data_frame_encoded_size": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "ufc_ack_frame_builder_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                                  ctypes.c_uint32]),
+    "ufc_ack_frame_builder_add": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int]),
+    "ufc_builder_size": (ctypes.c_size_t, [ctypes.c_void_p]),
+    "ufc_builder_build": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_int]),
+    "ufc_parse_batch_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                            ctypes.POINTER(ctypes.c_size_t), ctypes.c_int]),
+    "ufc_parse_batch_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.c_void_p, ctypes.c_void_p]),
 }
 SYMBOLS = tuple(_SIGNATURES)
+
+
+# Structs of include/uflow_frame_codec.h (layouts checked by tests/test_codec_cpu.py).
+class FrameInfo(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint8), ("ok", ctypes.c_uint8), ("aux", ctypes.c_uint8), ("crc_ok", ctypes.c_uint8),
+                ("f", ctypes.c_uint32 * 5), ("item_count", ctypes.c_uint32), ("item_first", ctypes.c_uint32)]
+
+
+class Item(ctypes.Structure):
+    _fields_ = [("id", ctypes.c_uint32), ("channel_id", ctypes.c_uint8), ("form", ctypes.c_uint8),
+                ("window_parent_lead", ctypes.c_uint16), ("channel_parent_lead", ctypes.c_uint16),
+                ("fragment_id", ctypes.c_uint16), ("fragment_id_last", ctypes.c_uint16), ("reserved", ctypes.c_uint16),
+                ("data_offset", ctypes.c_uint32), ("data_len", ctypes.c_uint32)]
+
+
+class Builder(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_void_p), ("cap", ctypes.c_size_t), ("len", ctypes.c_size_t),
+                ("count", ctypes.c_uint32), ("kind", ctypes.c_uint32)]
+
+
+class DatagramRef(ctypes.Structure):
+    _fields_ = [("sequence_id", ctypes.c_uint32), ("channel_id", ctypes.c_uint8), ("reserved", ctypes.c_uint8),
+                ("window_parent_lead", ctypes.c_uint16), ("channel_parent_lead", ctypes.c_uint16),
+                ("fragment_id", ctypes.c_uint16), ("fragment_id_last", ctypes.c_uint16),
+                ("data", ctypes.c_void_p), ("data_len", ctypes.c_size_t)]
 
 _lib = None
 

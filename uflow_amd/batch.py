@@ -103,6 +103,26 @@ class FrameCrcEngine:
                                           self._stream(stream)), "ufc_seal_batch_varlen")
         return crc_out
 
+    # ---- Frame::read past the gate, on the device (uflow_frame_codec.h) ----
+    def parse_varlen(self, data, offsets, valid, items_cap=None, stream=None):
+        """Batched Frame::read of a CSR batch after the CRC gate (`valid`, from crc_varlen).
+        Returns (infos uint8[n, 32], items uint8[items_cap, 24], items_used int64[1]) device tensors;
+        the byte rows are ufc_frame_info / ufc_item records (numpy views: uflow_amd.frame
+        FRAME_INFO_DTYPE / ITEM_DTYPE).  items_cap defaults to a bound no batch can exceed."""
+        n = offsets.numel() - 1
+        if offsets.dtype != torch.int64:
+            raise ValueError("offsets must be int64")
+        if items_cap is None:  # a datagram takes >= 6 bytes, an ack group 9
+            items_cap = max(1, data.numel() // 6)
+        infos = torch.empty((max(n, 0), 32), dtype=torch.uint8, device=self.device)
+        items = torch.empty((items_cap, 24), dtype=torch.uint8, device=self.device)
+        used = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self._check_dev(data, offsets, valid, infos, items, used)
+        check(lib().ufc_parse_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(valid), _ptr(infos),
+                                           _ptr(items), items_cap, _ptr(used), self._stream(stream)),
+              "ufc_parse_batch_varlen")
+        return infos, items, used
+
     # ---- host buffers (frames received into host memory) ----
     def validate_host_varlen(self, data: np.ndarray, offsets: np.ndarray):
         """numpy uint8 bytes + uint64/int64 offsets in host memory -> (crc uint32[n], valid uint8[n])."""

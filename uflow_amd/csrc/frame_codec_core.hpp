@@ -1,0 +1,172 @@
+// frame_codec_core.hpp -- the payload parse of Frame::read (everything after the CRC gate), written
+// once for the host codec (frame_codec.cpp) and the GPU batch parse (frame_parse.hip).
+//
+// Restates src/frame/serial/mod.rs:694-705 (dispatch on the frame id) and read_*_payload :54-434,
+// read_datagram :183-309.  A byte reader abstracts the frame: rd(i) = frame byte i (i < len).
+// Only bytes the reference reads are read, in the order it checks lengths, so a rejected frame
+// never reads past its end.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/uflow_frame_codec.h"
+
+namespace ufc_codec {
+
+#define UFC_HD __host__ __device__ __forceinline__
+
+constexpr uint32_t kMaxFrameSize = 1472;                  // src/lib.rs:286-294
+constexpr uint32_t kSynPayload = kMaxFrameSize - 5;       // serial/mod.rs:25
+constexpr uint32_t kDataPayloadHeader = 5;                // serial/mod.rs:41
+constexpr uint32_t kAckPayloadHeader = 10;                // serial/mod.rs:49
+
+template <class Rd>
+UFC_HD uint32_t be32(const Rd& rd, uint32_t i) {
+  return (rd(i) << 24) | (rd(i + 1) << 16) | (rd(i + 2) << 8) | rd(i + 3);
+}
+template <class Rd>
+UFC_HD uint32_t be16(const Rd& rd, uint32_t i) {
+  return (rd(i) << 8) | rd(i + 1);
+}
+
+// Parse the payload of a frame of `len` bytes (len >= 5) whose CRC gate passed.  Fills `info`
+// (kind, aux, f[], item_count) and, when items != nullptr, the first `cap` items.  Returns
+// whether Frame::read returns Some.
+template <class Rd>
+UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, ufc_item* items, uint32_t cap) {
+  const uint32_t plen = len - 5;  // payload = frame[1 .. len - 4]
+  auto p = [&](uint32_t i) -> uint32_t { return rd(1 + i); };
+  auto p32 = [&](uint32_t i) -> uint32_t { return be32(rd, 1 + i); };
+  auto p16 = [&](uint32_t i) -> uint32_t { return be16(rd, 1 + i); };
+  info.item_count = 0;
+  switch (info.kind) {
+    case UFC_FRAME_HANDSHAKE_SYN:  // :54-87
+      if (plen != kSynPayload) return false;
+      info.aux = (uint8_t)p(0);
+      info.f[0] = p32(1); info.f[1] = p32(5); info.f[2] = p32(9); info.f[3] = p32(13);
+      return true;
+    case UFC_FRAME_HANDSHAKE_SYN_ACK:  // :89-126
+      if (plen != 20) return false;
+      info.f[0] = p32(0); info.f[1] = p32(4); info.f[2] = p32(8); info.f[3] = p32(12); info.f[4] = p32(16);
+      return true;
+    case UFC_FRAME_HANDSHAKE_ACK:  // :128-141
+      if (plen != 4) return false;
+      info.f[0] = p32(0);
+      return true;
+    case UFC_FRAME_HANDSHAKE_ERROR: {  // :143-165
+      if (plen != 5) return false;
+      const uint32_t e = p(4);
+      if (e > 2) return false;
+      info.f[0] = p32(0);
+      info.aux = (uint8_t)e;
+      return true;
+    }
+    case UFC_FRAME_DISCONNECT:      // :167-173
+    case UFC_FRAME_DISCONNECT_ACK:  // :175-181
+      return plen == 0;
+    case UFC_FRAME_DATA: {  // :311-340
+      if (plen < kDataPayloadHeader) return false;
+      info.f[0] = p32(0);
+      const uint32_t b4 = p(4);
+      info.aux = (uint8_t)(b4 >> 7);
+      const uint32_t cnt = b4 & 0x7F;
+      uint32_t pos = kDataPayloadHeader;
+      for (uint32_t k = 0; k < cnt; k++) {  // read_datagram, :183-309
+        const uint32_t rem = plen - pos;
+        if (rem < 6) return false;
+        const uint32_t b0 = p(pos);
+        ufc_item it{};
+        uint32_t hs, dl;
+        if ((b0 & 0x80) == 0) {  // micro (:190-229)
+          hs = 6;
+          dl = b0 & 0x3F;
+          if (rem < hs + dl) return false;
+          const uint32_t b1 = p(pos + 1), b4d = p(pos + 4);
+          it.channel_id = (uint8_t)(((b4d >> 2) & 0x20) | ((b0 >> 2) & 0x10) | (b1 & 0x0F));
+          it.id = ((b1 & 0xF0) << 12) | (p(pos + 2) << 8) | p(pos + 3);
+          it.window_parent_lead = (uint16_t)(b4d & 0x7F);
+          it.channel_parent_lead = (uint16_t)p(pos + 5);
+          it.form = 0;
+        } else if ((b0 & 0x40) == 0) {  // small (:230-268)
+          hs = 9;
+          dl = p(pos + 1);
+          if (rem < hs + dl) return false;
+          it.channel_id = (uint8_t)(b0 & 0x3F);
+          it.id = ((p(pos + 2) & 0x0F) << 16) | (p(pos + 3) << 8) | p(pos + 4);
+          it.window_parent_lead = (uint16_t)p16(pos + 5);
+          it.channel_parent_lead = (uint16_t)p16(pos + 7);
+          it.form = 1;
+        } else {  // large (:269-308)
+          hs = 14;
+          dl = p16(pos + 1);
+          if (rem < hs + dl) return false;
+          it.channel_id = (uint8_t)(b0 & 0x3F);
+          it.id = ((p(pos + 3) & 0x0F) << 16) | (p(pos + 4) << 8) | p(pos + 5);
+          it.window_parent_lead = (uint16_t)p16(pos + 6);
+          it.channel_parent_lead = (uint16_t)p16(pos + 8);
+          it.fragment_id = (uint16_t)p16(pos + 10);
+          it.fragment_id_last = (uint16_t)p16(pos + 12);
+          it.form = 2;
+        }
+        it.data_offset = 1 + pos + hs;
+        it.data_len = dl;
+        if (items && k < cap) items[k] = it;
+        pos += hs + dl;
+      }
+      if (pos != plen) return false;  // :335-337
+      info.item_count = cnt;
+      return true;
+    }
+    case UFC_FRAME_SYNC: {  // :342-367
+      if (plen != 9) return false;
+      const uint32_t mode = p(0);
+      info.aux = (uint8_t)(mode & 3u);
+      info.f[0] = (mode & 1u) ? p32(1) : 0u;
+      info.f[1] = (mode & 2u) ? p32(5) : 0u;
+      return true;
+    }
+    case UFC_FRAME_ACK: {  // :369-434
+      if (plen < kAckPayloadHeader) return false;
+      const uint32_t cnt = p16(8);
+      // each group needs 9 bytes (:395-397, :412-417) and nothing may remain (:425-427)
+      if (plen - kAckPayloadHeader != UFC_ACK_GROUP_SIZE * cnt) return false;
+      info.f[0] = p32(0);
+      info.f[1] = p32(4);
+      if (items) {
+        for (uint32_t k = 0; k < cnt && k < cap; k++) {
+          const uint32_t o = kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
+          ufc_item it{};
+          it.id = p32(o);
+          it.data_offset = p32(o + 4);  // bitfield
+          it.channel_id = (uint8_t)(p(o + 8) != 0 ? 1 : 0);
+          it.form = 3;
+          items[k] = it;
+        }
+      }
+      info.item_count = cnt;
+      return true;
+    }
+    default:
+      return false;  // unknown id (:704)
+  }
+}
+
+// Frame::read given the CRC gate's verdict for the frame (crc_ok = len >= 5 && trailer matches).
+template <class Rd>
+UFC_HD bool read_frame(const Rd& rd, uint32_t len, bool crc_ok, ufc_frame_info& info, ufc_item* items,
+                       uint32_t cap) {
+  info.kind = len >= 1 ? (uint8_t)rd(0) : (uint8_t)0xFF;
+  info.ok = 0;
+  info.aux = 0;
+  info.crc_ok = (crc_ok && len >= 5) ? 1 : 0;
+  for (int i = 0; i < 5; i++) info.f[i] = 0;
+  info.item_count = 0;
+  if (!info.crc_ok) return false;
+  const bool ok = parse_payload(rd, len, info, items, cap);
+  if (!ok) info.item_count = 0;
+  info.ok = ok ? 1 : 0;
+  return ok;
+}
+
+}  // namespace ufc_codec

@@ -13,9 +13,11 @@
 #include <new>
 #include <vector>
 
+#include "../../include/uflow_frame_codec.h"
 #include "../../include/uflow_frame_crc.h"
 #include "crc_math.hpp"
 #include "frame_crc_kernels.hpp"
+#include "frame_parse.hpp"
 
 struct ufc_ctx {
   int device = -1;
@@ -40,6 +42,9 @@ struct ufc_ctx {
   // concurrent launches on different streams do not share counters (up to kCtrSlots in flight).
   uint32_t* d_ctr = nullptr;
   std::atomic<uint32_t> ctr_seq{0};
+  // Batch parse scratch (item counts, first indices, scan temporaries): grow-only.
+  void* d_parse = nullptr;
+  size_t d_parse_cap = 0;
 };
 
 constexpr uint32_t kCtrSlots = 64;
@@ -322,6 +327,7 @@ int ufc_ctx_destroy(ufc_ctx* ctx) {
     if (ctx->d_chain) (void)hipFree(ctx->d_chain);
     if (ctx->d_nib) (void)hipFree(ctx->d_nib);
     if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
+    if (ctx->d_parse) (void)hipFree(ctx->d_parse);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_off) (void)hipFree(ctx->d_off);
     if (ctx->d_crc) (void)hipFree(ctx->d_crc);
@@ -503,6 +509,30 @@ int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_
   }
   for (hipStream_t s : ctx->streams)
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e);
+  return UFC_OK;
+}
+
+int ufc_parse_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
+                           const uint8_t* d_valid, ufc_frame_info* d_infos, ufc_item* d_items, size_t items_cap,
+                           uint64_t* d_items_used, void* stream) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!d_bytes || !d_offsets || !d_valid || !d_infos || n >= ((size_t)1 << 31)) return UFC_ERR_INVALID_ARG;
+  DeviceGuard g(ctx->device);
+  hipError_t e;
+  const size_t need = ufc_dev::parse_scratch_bytes(n);
+  if (ctx->d_parse_cap < need) {  // grows on the first (or a larger) batch only
+    if (ctx->d_parse && (e = hipStreamSynchronize((hipStream_t)stream)) != hipSuccess) return hip_fail(ctx, e);
+    if (ctx->d_parse) (void)hipFree(ctx->d_parse);
+    ctx->d_parse = nullptr;
+    ctx->d_parse_cap = 0;
+    if ((e = hipMalloc(&ctx->d_parse, need)) != hipSuccess) return hip_fail(ctx, e);
+    ctx->d_parse_cap = need;
+  }
+  ufc_dev::ParseArgs a{d_bytes, d_offsets, (uint64_t)n, d_valid, d_infos, d_items, (uint64_t)(d_items ? items_cap : 0),
+                       d_items_used};
+  if ((e = ufc_dev::parse_batch(a, ctx->d_parse, ctx->d_parse_cap, (hipStream_t)stream)) != hipSuccess)
+    return hip_fail(ctx, e);
   return UFC_OK;
 }
 
