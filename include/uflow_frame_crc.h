@@ -12,8 +12,10 @@
  *   ufc_crc_batch_varlen      (src/server/mod.rs:597-601, src/client/mod.rs:618-622), batched on the GPU
  *   ufc_seal_batch_fixed / <- many calls of the seal above, one per emitted frame
  *   ufc_seal_batch_varlen     (src/half_connection/emit.rs:114-125, 205-211), batched on the GPU
+ *   ufc_crc_batch_pairs       the gate over frames given as (start, end) pairs (any gapped layout)
  *   ufc_validate_host_varlen  the same gate for frames that start and end in host memory
- *                             (a UDP receive buffer): H2D copy + GPU CRC + D2H copy
+ *   ufc_validate_host_slots   (a UDP receive buffer): H2D copy + GPU CRC + D2H copy; _slots takes the
+ *                             recvmmsg layout (fixed-size slots + lengths) of the receive loops
  *
  * Conventions (mirroring the reference):
  *   - All buffers are caller-owned; nothing is retained after a call returns (device calls:
@@ -84,11 +86,21 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
 int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
                           uint32_t* d_crc_out, void* stream);
 
+/* Frame i occupies d_bytes[d_pairs[2i] .. d_pairs[2i+1]) (start <= end <= bytes_len): any
+ * gapped layout, e.g. datagrams received into fixed-size slots.  Validate only. */
+int ufc_crc_batch_pairs(ufc_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, const uint64_t* d_pairs, size_t n,
+                        uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream);
+
 /* ---- host buffers in, host buffers out (the receive path of SURVEY.md config 5) ----
  * Copies the frames through pinned staging buffers owned by the context, runs the batched
  * gate on the device and copies crc/valid back; synchronous.  h_offsets as above. */
 int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
                              uint32_t* h_crc_out, uint8_t* h_valid_out);
+/* The batched receive loop's layout: datagram i was received (recvmmsg) into the slot
+ * h_slots[i*slot_stride ..] and is h_lens[i] <= slot_stride bytes long.  Same staging as above;
+ * no host-side compaction. */
+int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
+                            size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out);
 
 #ifdef __cplusplus
 }

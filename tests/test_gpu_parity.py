@@ -297,3 +297,45 @@ def test_parse_varlen_vs_host_parse_large(engine):
     k = int(used.cpu()[0])
     assert k == ref_items.size
     assert np.array_equal(items[:k].cpu().numpy().view(ITEM_DTYPE).reshape(-1), ref_items)
+
+
+def test_pairs_gapped_layout(engine):
+    """(start, end) pairs over a buffer with gaps and out-of-order frames."""
+    rng = np.random.default_rng(61)
+    lens = rng.integers(0, 1700, size=20_000)
+    gaps = rng.integers(0, 40, size=lens.size)
+    starts = np.cumsum(np.concatenate([[0], (lens + gaps)[:-1]])) + gaps[0]
+    buf = _rand_bytes(rng, int(starts[-1] + lens[-1]) + 3)
+    for s, l in zip(starts, lens):
+        if l >= 4:
+            fr = bytearray(buf[s:s + l].tobytes())
+            oracle.frame_seal(fr)
+            buf[s:s + l] = np.frombuffer(bytes(fr), np.uint8)
+    for i in range(0, lens.size, 41):
+        if lens[i]:
+            buf[starts[i] + rng.integers(0, lens[i])] ^= 8
+    perm = rng.permutation(lens.size)
+    pairs = np.stack([starts[perm], starts[perm] + lens[perm]], axis=1).astype(np.int64)
+    ref = [oracle.frame_validate(buf[a:b].tobytes()) for a, b in pairs]
+    crc, valid = engine.crc_pairs(torch.from_numpy(buf).to(DEV), torch.from_numpy(pairs).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(valid.cpu().numpy(), np.array([int(v) for v, _ in ref], np.uint8))
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), np.array([c for _, c in ref], np.uint32))
+
+
+def test_host_slots(engine):
+    """The receive loop's recvmmsg layout: fixed 1472-B slots with per-datagram lengths."""
+    rng = np.random.default_rng(62)
+    n, stride = 70_001, 1472
+    lens = rng.integers(5, stride + 1, size=n).astype(np.uint32)
+    slots = _rand_bytes(rng, n * stride)
+    for i in range(n):
+        fr = bytearray(slots[i * stride:i * stride + lens[i]].tobytes())
+        oracle.frame_seal(fr)
+        slots[i * stride:i * stride + lens[i]] = np.frombuffer(bytes(fr), np.uint8)
+    slots[np.arange(0, n, 101) * stride + 2] ^= 0x40
+    crc, valid = engine.validate_host_slots(slots, stride, lens)
+    ref = [oracle.frame_validate(slots[i * stride:i * stride + lens[i]].tobytes()) for i in range(0, n, 7)]
+    assert np.array_equal(valid[::7], np.array([int(v) for v, _ in ref], np.uint8))
+    assert np.array_equal(crc[::7], np.array([c for _, c in ref], np.uint32))
+    assert int(valid.sum()) == n - len(range(0, n, 101))

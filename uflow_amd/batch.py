@@ -103,6 +103,20 @@ class FrameCrcEngine:
                                           self._stream(stream)), "ufc_seal_batch_varlen")
         return crc_out
 
+    def crc_pairs(self, data, pairs, crc_out=None, valid_out=None, stream=None):
+        """pairs: int64 tensor [n, 2] of (start, end) byte offsets into data (any gapped layout)."""
+        n = pairs.shape[0]
+        if pairs.dtype != torch.int64:
+            raise ValueError("pairs must be int64")
+        if crc_out is None:
+            crc_out = torch.empty(n, dtype=torch.int32, device=self.device)
+        if valid_out is None:
+            valid_out = torch.empty(n, dtype=torch.uint8, device=self.device)
+        self._check_dev(data, pairs, crc_out, valid_out)
+        check(lib().ufc_crc_batch_pairs(self._ctx, _ptr(data), data.numel(), _ptr(pairs), n, _ptr(crc_out),
+                                        _ptr(valid_out), self._stream(stream)), "ufc_crc_batch_pairs")
+        return crc_out, valid_out
+
     # ---- Frame::read past the gate, on the device (uflow_frame_codec.h) ----
     def parse_varlen(self, data, offsets, valid, items_cap=None, stream=None):
         """Batched Frame::read of a CSR batch after the CRC gate (`valid`, from crc_varlen).
@@ -124,6 +138,17 @@ class FrameCrcEngine:
         return infos, items, used
 
     # ---- host buffers (frames received into host memory) ----
+    def validate_host_slots(self, slots: np.ndarray, slot_stride: int, lens: np.ndarray):
+        """Datagrams received into fixed-size slots (recvmmsg layout) -> (crc uint32[n], valid uint8[n])."""
+        slots = np.ascontiguousarray(slots, dtype=np.uint8)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        n = lens.size
+        crc = np.empty(n, dtype=np.uint32)
+        valid = np.empty(n, dtype=np.uint8)
+        check(lib().ufc_validate_host_slots(self._ctx, slots.ctypes.data, slot_stride, lens.ctypes.data, n,
+                                            crc.ctypes.data, valid.ctypes.data), "ufc_validate_host_slots")
+        return crc, valid
+
     def validate_host_varlen(self, data: np.ndarray, offsets: np.ndarray):
         """numpy uint8 bytes + uint64/int64 offsets in host memory -> (crc uint32[n], valid uint8[n])."""
         data = np.ascontiguousarray(data, dtype=np.uint8)

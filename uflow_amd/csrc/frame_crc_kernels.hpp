@@ -46,8 +46,9 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, bool dyn);
 // Lean variable-length kernel (CSR offsets, any frame lengths; frames of 4..1532 B on the fast
 // path, the rest byte-wise after the main loop).  Set indices are 30-bit: a launch covers fewer
 // than 2^32 frames (host-chunked).
-// abl != 0: ablation variants of tuning builds (validate only).
-const void* varlen_kernel_symbol(bool seal, int abl);
+// pairs: frames given as (start, end) pairs instead of CSR offsets (KernelParams::offsets holds
+// 2n words, frame_len the buffer length).  abl != 0: ablation variants of tuning builds.
+const void* varlen_kernel_symbol(bool seal, bool pairs, int abl);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

@@ -93,7 +93,9 @@ constexpr int kAuxNT = 2;               // cache policy bits of the load: nt (st
 
 // ABL (tuning builds only; results meaningless): bit 0 = loads + XOR fold, no CRC; bit 1 = CRC of
 // register data, no block loads (offsets and geometry kept).
-template <bool SEAL, int ABL>
+// PAIRS: frame i = bytes[pairs[2i] .. pairs[2i+1]) (p.offsets holds the 2n pairs, p.frame_len the
+// buffer's byte length): any gapped layout, e.g. datagrams received into fixed-size slots.
+template <bool SEAL, bool PAIRS, int ABL>
 __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelParams p) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const StageRegs sr = stage_load(p);
@@ -114,13 +116,23 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   };
   // Sets 0..3 of each wave are static (lo + 16i + wid); the rest are claimed.
   auto claim_set = [&](uint32_t v) -> uint32_t { return q_lo + 4 * wpb + __builtin_amdgcn_readfirstlane(v); };
-  // offsets[4q + g + (col & 1)] (clamped): even lanes get the frame's start, odd lanes its end.
+  // offsets[4q + g + (col & 1)] (clamped), or pairs[2(4q + g) + (col & 1)]: even lanes get the
+  // frame's start, odd lanes its end.
   auto load_off = [&](uint32_t q) -> uint64_t {
+    if (PAIRS) {
+      const uint64_t f = min(4 * (uint64_t)min(q, nsets - 1) + (uint64_t)L.grp, nfr - 1);
+      return *as_global<g_u64>(p.offsets + 2 * f + (uint64_t)(L.col & 1));
+    }
     const uint64_t i = 4 * (uint64_t)min(q, nsets - 1) + (uint64_t)L.grp + (uint64_t)(L.col & 1);
     return *as_global<g_u64>(p.offsets + (i < nfr ? i : nfr));
   };
+  auto frame_bounds = [&](uint64_t f, uint64_t& a, uint64_t& b) {
+    a = PAIRS ? p.offsets[2 * f] : p.offsets[f];
+    b = PAIRS ? p.offsets[2 * f + 1] : p.offsets[f + 1];
+  };
   const uint32_t lane16 = 16u * (uint32_t)L.col;
-  const uint64_t buf_end = *as_global<g_u64>(p.offsets + nfr);  // end of the batch's bytes
+  // end of the batch's bytes (CSR: the last offset; pairs: the buffer length)
+  const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets + nfr);
 
   // Geometry of set q from its offsets: lane offset of block 0 (voff0), packed per-lane geometry,
   // the set's scalar base and uniform meta.  A set that is not live (past the range, or slow)
@@ -265,8 +277,9 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   auto slow_set = [&](uint32_t q) {
     const uint64_t fr = 4 * (uint64_t)q + (uint64_t)L.grp;
     const uint64_t f = fr < nfr ? fr : nfr - 1;
-    const uint64_t a = p.offsets[f], b = p.offsets[f + 1];
-    const FrameDesc d = make_desc(a, b - a);
+    uint64_t a, b;
+    frame_bounds(f, a, b);
+    const FrameDesc d = make_desc(a, b >= a ? b - a : 0);
     const int nb = max(max(__builtin_amdgcn_readlane(d.J, 0), __builtin_amdgcn_readlane(d.J, 16)),
                        max(__builtin_amdgcn_readlane(d.J, 32), __builtin_amdgcn_readlane(d.J, 48)));
     Chains ce{0u, 0u, 0u, 0u, 0u};
@@ -380,20 +393,24 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   }
 }
 
-template __global__ void frame_crc_varlen_kernel<false, 0>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<true, 0>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, false, 0>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<true, false, 0>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, true, 0>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<true, true, 0>(const KernelParams);
 #ifdef UFC_TUNING
-template __global__ void frame_crc_varlen_kernel<false, 1>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, 2>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, false, 1>(const KernelParams);
+template __global__ void frame_crc_varlen_kernel<false, false, 2>(const KernelParams);
 #endif
 
-const void* varlen_kernel_symbol(bool seal, int abl) {
+const void* varlen_kernel_symbol(bool seal, bool pairs, int abl) {
 #ifdef UFC_TUNING
-  if (!seal && abl == 1) return (const void*)frame_crc_varlen_kernel<false, 1>;
-  if (!seal && abl == 2) return (const void*)frame_crc_varlen_kernel<false, 2>;
+  if (!seal && !pairs && abl == 1) return (const void*)frame_crc_varlen_kernel<false, false, 1>;
+  if (!seal && !pairs && abl == 2) return (const void*)frame_crc_varlen_kernel<false, false, 2>;
 #endif
   if (abl != 0) return nullptr;
-  return seal ? (const void*)frame_crc_varlen_kernel<true, 0> : (const void*)frame_crc_varlen_kernel<false, 0>;
+  if (pairs)
+    return seal ? (const void*)frame_crc_varlen_kernel<true, true, 0> : (const void*)frame_crc_varlen_kernel<false, true, 0>;
+  return seal ? (const void*)frame_crc_varlen_kernel<true, false, 0> : (const void*)frame_crc_varlen_kernel<false, false, 0>;
 }
 
 }  // namespace ufc_dev

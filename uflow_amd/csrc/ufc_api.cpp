@@ -181,12 +181,12 @@ bool lean_varlen() {
   return !(k && std::strcmp(k, "generic") == 0);
 }
 
-int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
+int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream, bool pairs = false) {
   int abl = 0;
 #ifdef UFC_TUNING
   if (const char* ab = std::getenv("UFC_VL_ABL")) abl = std::atoi(ab);
 #endif
-  const void* fn = ufc_dev::varlen_kernel_symbol(seal, abl);
+  const void* fn = ufc_dev::varlen_kernel_symbol(seal, pairs, pairs ? 0 : abl);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain;
   kp.nib_img = ctx->d_nib;
@@ -199,7 +199,7 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
   for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
-    c.offsets = kp.offsets + f0;
+    c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
     const uint32_t slot = ctx->ctr_seq.fetch_add(1) % kCtrSlots;
@@ -501,6 +501,96 @@ int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_
     kp.crc_out = dcrc;
     kp.valid_out = dval;
     int rc = lean_varlen() ? launch_lean_varlen(ctx, false, kp, s) : launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, s);
+    if (rc != UFC_OK) return rc;
+    if (h_crc_out && (e = hipMemcpyAsync(h_crc_out + a, dcrc, nf * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(ctx, e);
+    if (h_valid_out && (e = hipMemcpyAsync(h_valid_out + a, dval, nf, hipMemcpyDeviceToHost, s)) != hipSuccess)
+      return hip_fail(ctx, e);
+  }
+  for (hipStream_t s : ctx->streams)
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e);
+  return UFC_OK;
+}
+
+int ufc_crc_batch_pairs(ufc_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, const uint64_t* d_pairs, size_t n,
+                        uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!d_bytes || !d_pairs || (!d_crc_out && !d_valid_out)) return UFC_ERR_INVALID_ARG;
+  ufc_dev::KernelParams kp{};
+  kp.bytes = d_bytes;
+  kp.offsets = d_pairs;
+  kp.frame_len = bytes_len;
+  kp.nframes = n;
+  kp.crc_out = d_crc_out;
+  kp.valid_out = d_valid_out;
+  DeviceGuard g(ctx->device);
+  return launch_lean_varlen(ctx, false, kp, (hipStream_t)stream, true);
+}
+
+int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
+                            size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!h_slots || !h_lens || slot_stride == 0 || (!h_crc_out && !h_valid_out)) return UFC_ERR_INVALID_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (h_lens[i] > slot_stride) return UFC_ERR_INVALID_ARG;
+  DeviceGuard g(ctx->device);
+  hipError_t e;
+  for (hipStream_t& s : ctx->streams)
+    if (!s && (e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return hip_fail(ctx, e);
+  // Chunks of whole slots (<= 64 MB); chunk k on stream/slot k & 1, as ufc_validate_host_varlen.
+  const size_t per = std::max<size_t>(1, std::min<size_t>((size_t)1 << 20, ((size_t)64 << 20) / slot_stride));
+  const size_t cf = std::min(per, n);
+  const size_t cb = cf * slot_stride;
+  if (ctx->d_stage_cap < 2 * cb + 64) {
+    if (ctx->d_stage) (void)hipFree(ctx->d_stage);
+    ctx->d_stage = nullptr;
+    ctx->d_stage_cap = 0;
+    if ((e = hipMalloc(&ctx->d_stage, 2 * cb + 64)) != hipSuccess) return hip_fail(ctx, e);
+    ctx->d_stage_cap = 2 * cb + 64;
+  }
+  if (ctx->d_off_cap < 4 * cf) {
+    if (ctx->d_off) (void)hipFree(ctx->d_off);
+    if (ctx->h_off_pinned) (void)hipHostFree(ctx->h_off_pinned);
+    ctx->d_off = nullptr;
+    ctx->h_off_pinned = nullptr;
+    ctx->d_off_cap = ctx->h_off_cap = 0;
+    if ((e = hipMalloc(&ctx->d_off, 4 * cf * 8)) != hipSuccess) return hip_fail(ctx, e);
+    if ((e = hipHostMalloc(&ctx->h_off_pinned, 4 * cf * 8, hipHostMallocDefault)) != hipSuccess) return hip_fail(ctx, e);
+    ctx->d_off_cap = ctx->h_off_cap = 4 * cf;
+  }
+  if (ctx->d_out_cap < 2 * cf) {
+    if (ctx->d_crc) (void)hipFree(ctx->d_crc);
+    if (ctx->d_valid) (void)hipFree(ctx->d_valid);
+    ctx->d_crc = nullptr;
+    ctx->d_valid = nullptr;
+    ctx->d_out_cap = 0;
+    if ((e = hipMalloc(&ctx->d_crc, 2 * cf * 4)) != hipSuccess) return hip_fail(ctx, e);
+    if ((e = hipMalloc(&ctx->d_valid, 2 * cf)) != hipSuccess) return hip_fail(ctx, e);
+    ctx->d_out_cap = 2 * cf;
+  }
+  size_t k = 0;
+  for (size_t a = 0; a < n; a += cf, k++) {
+    const int slot = (int)(k & 1);
+    hipStream_t s = ctx->streams[slot];
+    const size_t nf = std::min(cf, n - a);
+    uint8_t* dst = ctx->d_stage + (size_t)slot * (cb + 32);
+    uint64_t* hp = ctx->h_off_pinned + (size_t)slot * 2 * cf;
+    uint64_t* dp = ctx->d_off + (size_t)slot * 2 * cf;
+    if (k >= 2 && (e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e);
+    for (size_t i = 0; i < nf; i++) {
+      hp[2 * i] = (uint64_t)i * slot_stride;
+      hp[2 * i + 1] = (uint64_t)i * slot_stride + h_lens[a + i];
+    }
+    // the last slot only up to its datagram's end (the slab may end there)
+    const size_t bytes = (nf - 1) * slot_stride + h_lens[a + nf - 1];
+    if (bytes && (e = hipMemcpyAsync(dst, h_slots + a * slot_stride, bytes, hipMemcpyHostToDevice, s)) != hipSuccess)
+      return hip_fail(ctx, e);
+    if ((e = hipMemcpyAsync(dp, hp, nf * 16, hipMemcpyHostToDevice, s)) != hipSuccess) return hip_fail(ctx, e);
+    uint32_t* dcrc = ctx->d_crc + (size_t)slot * cf;
+    uint8_t* dval = ctx->d_valid + (size_t)slot * cf;
+    int rc = ufc_crc_batch_pairs(ctx, dst, bytes, dp, nf, dcrc, dval, s);
     if (rc != UFC_OK) return rc;
     if (h_crc_out && (e = hipMemcpyAsync(h_crc_out + a, dcrc, nf * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
       return hip_fail(ctx, e);
