@@ -88,6 +88,11 @@ typedef struct ufc_item {
  * (info->item_count says how many the frame holds; UFC_ERR_NOMEM if items_cap is smaller). */
 int ufc_frame_read(const uint8_t* frame, size_t len, ufc_frame_info* info, ufc_item* items, size_t items_cap);
 
+/* The rest of Frame::read after an external CRC gate (e.g. the batched GPU gate): crc_ok is the
+ * gate's verdict for this frame.  Returns and fills as ufc_frame_read. */
+int ufc_frame_parse(const uint8_t* frame, size_t len, int crc_ok, ufc_frame_info* info, ufc_item* items,
+                    size_t items_cap);
+
 /* Fixed-size frames (every kind but data and ack) from info; writes the BE32 CRC trailer when
  * seal != 0, else 4 zero bytes (for a batched seal on the GPU).  Returns the frame length, 0 if
  * cap is too small or the kind is data/ack/unknown. */

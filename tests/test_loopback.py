@@ -1,0 +1,45 @@
+"""The loopback harness (tools/loopback/ufc_loopback, BASELINE.json configs 1 and 5): frames built
+by the native builders, sent over UDP 127.0.0.1, received in batches (recvmmsg), gated and parsed.
+CPU: the echo plumbing (examples/echo_server.rs + echo_client.rs) and a short stream with the CPU
+gate; GPU: the same stream with the GPU gate (ufc_validate_host_slots) in the receive path."""
+import json
+import os
+import random
+import subprocess
+
+import pytest
+
+from uflow_amd._build import LOOPBACK_BIN, build_tools
+
+
+def _run(args, timeout=120):
+    build_tools()
+    port = str(random.randrange(20000, 60000))
+    r = subprocess.run([LOOPBACK_BIN, "--port", port] + args, capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    return json.loads(lines[-1])
+
+
+def test_echo_plumbing():
+    j = _run(["--echo"])
+    assert j["echoes_ok"] == j["messages"] == 10
+
+
+def _check_stream(j, n, every):
+    assert j["payload_mismatch"] == 0
+    assert j["received"] > 0 and j["valid"] + j["invalid"] == j["received"]
+    assert j["parsed"] == j["valid"]
+    if j["received"] == n:  # nothing dropped by the socket: exactly the corrupted frames fail
+        assert j["invalid"] == n // every
+
+
+def test_stream_cpu_gate():
+    n = 100_000
+    _check_stream(_run(["--gate", "cpu", "--frames", str(n), "--corrupt-every", "997"]), n, 997)
+
+
+@pytest.mark.gpu
+def test_stream_gpu_gate():
+    n = 200_000
+    _check_stream(_run(["--gate", "gpu", "--frames", str(n), "--corrupt-every", "997"]), n, 997)

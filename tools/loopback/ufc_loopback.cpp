@@ -1,0 +1,420 @@
+// ufc_loopback -- uflow frames over UDP loopback with the batched CRC gate in the receive path.
+//
+// Two modes (BASELINE.json configs 1 and 5):
+//   --echo        a restatement of examples/echo_server.rs + echo_client.rs as frame plumbing:
+//                 the client sends data frames carrying "Hello world!" packets to 127.0.0.1:8888,
+//                 the server gates them on the CPU (ufc_frame_read = Frame::read), echoes each
+//                 packet on channel 0 and its reverse on channel 1 (echo_server.rs:23-32), and the
+//                 client gates and checks the echoes.  No connection protocol: frames only.
+//   (default)     tests/ideal_transfer.rs at saturation: a sender thread streams data frames of one
+//                 MAX_FRAGMENT_SIZE (1448 B) datagram each (1472-B frames, 4 channels) with
+//                 sendmmsg; the receiver takes batches with recvmmsg into fixed 1472-B slots (pinned
+//                 host memory) and hands each batch to a worker that runs the CRC gate -- on the GPU
+//                 (ufc_validate_host_slots: H2D + kernel + D2H) or on the CPU (--gate cpu) -- then
+//                 the rest of Frame::read (ufc_frame_parse) and checks every payload byte.  The
+//                 reference does one recv_from + Frame::read per datagram (server/mod.rs:591-602).
+// Output: one JSON line (frames/s and GB/s of frame bytes received, gated and parsed).
+#include <arpa/inet.h>
+#include <hip/hip_runtime.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/uflow_frame_codec.h"
+
+namespace {
+
+constexpr size_t kFrame = 1472;              // MAX_FRAME_SIZE (src/lib.rs:294)
+constexpr size_t kFragment = 1448;           // MAX_FRAGMENT_SIZE (src/lib.rs:297)
+constexpr int kChannels = 4;                 // tests/ideal_transfer.rs:10
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int udp_socket(uint16_t port, bool bind_it, int rcvbuf) {
+  int fd = socket(AF_INET, SOCK_DGRAM, 0);
+  if (fd < 0) {
+    perror("socket");
+    exit(2);
+  }
+  if (rcvbuf) setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &rcvbuf, sizeof(rcvbuf));
+  int sndbuf = 8 << 20;
+  setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sndbuf, sizeof(sndbuf));
+  if (bind_it) {
+    sockaddr_in a{};
+    a.sin_family = AF_INET;
+    a.sin_port = htons(port);
+    a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+    if (bind(fd, (sockaddr*)&a, sizeof(a)) != 0) {
+      perror("bind");
+      exit(2);
+    }
+  }
+  return fd;
+}
+
+sockaddr_in loopback(uint16_t port) {
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons(port);
+  a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+  return a;
+}
+
+void set_timeout(int fd, int ms) {
+  timeval tv{ms / 1000, (ms % 1000) * 1000};
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+}
+
+// Payload byte i of packet p on channel c (ideal_transfer.rs:76-84 puts the channel and a BE
+// packet id first; the rest is a pattern the receiver can recompute).
+inline uint8_t payload_byte(uint32_t c, uint32_t p, size_t i) {
+  if (i == 0) return (uint8_t)c;
+  if (i < 5) return (uint8_t)(p >> (8 * (4 - i)));
+  return (uint8_t)(p * 131u + (uint32_t)i * 7u + c);
+}
+
+// One frame of the stream: data frame `seq` = packet seq / 4 of channel seq % 4.
+size_t build_stream_frame(uint8_t* out, uint32_t seq, bool seal) {
+  const uint32_t c = seq % kChannels, p = seq / kChannels;
+  static thread_local std::vector<uint8_t> pay(kFragment);
+  for (size_t i = 0; i < kFragment; i++) pay[i] = payload_byte(c, p, i);
+  ufc_builder b;
+  ufc_data_frame_builder_init(&b, out, kFrame, seq, 0);
+  ufc_datagram_ref d{};
+  d.sequence_id = p & 0xFFFFF;
+  d.channel_id = (uint8_t)c;
+  d.data = pay.data();
+  d.data_len = kFragment;
+  if (ufc_data_frame_builder_add(&b, &d) != UFC_OK) abort();
+  return ufc_builder_build(&b, seal ? 1 : 0);
+}
+
+struct Args {
+  bool echo = false;
+  bool gpu = true;
+  uint64_t frames = 2000000;
+  int batch = 4096;
+  uint16_t port = 8888;
+  uint64_t corrupt_every = 0;  // flip one bit in every k-th frame (must be rejected)
+  bool verify = true;
+};
+
+// ---------------- config 1: echo plumbing ----------------
+int run_echo(const Args& a) {
+  const int srv = udp_socket(a.port, true, 1 << 20);
+  const int cli = udp_socket(0, false, 1 << 20);
+  set_timeout(srv, 2000);
+  set_timeout(cli, 2000);
+  const int kMsgs = 10;
+  std::atomic<int> served{0};
+  std::thread server([&] {
+    uint8_t buf[kFrame], out[kFrame];
+    ufc_frame_info info;
+    ufc_item items[UFC_DATA_FRAME_MAX_DATAGRAM_COUNT];
+    for (int k = 0; k < kMsgs; k++) {
+      sockaddr_in from{};
+      socklen_t fl = sizeof(from);
+      const ssize_t n = recvfrom(srv, buf, sizeof(buf), 0, (sockaddr*)&from, &fl);
+      if (n < 0) return;
+      if (ufc_frame_read(buf, (size_t)n, &info, items, UFC_DATA_FRAME_MAX_DATAGRAM_COUNT) != 1 ||
+          info.kind != UFC_FRAME_DATA)
+        continue;  // Frame::read returned None: dropped silently (server/mod.rs:598)
+      for (uint32_t j = 0; j < info.item_count; j++) {
+        const uint8_t* msg = buf + items[j].data_offset;
+        const uint32_t len = items[j].data_len;
+        std::string s((const char*)msg, len), r(s.rbegin(), s.rend());
+        printf("[server] received \"%s\"\n", s.c_str());
+        ufc_builder b;
+        ufc_data_frame_builder_init(&b, out, sizeof(out), info.f[0], 0);
+        ufc_datagram_ref d0{};  // echo on channel 0 (echo_server.rs:29)
+        d0.sequence_id = items[j].id;
+        d0.channel_id = 0;
+        d0.data = msg;
+        d0.data_len = len;
+        ufc_datagram_ref d1 = d0;  // reversed on channel 1 (echo_server.rs:32)
+        d1.channel_id = 1;
+        d1.data = (const uint8_t*)r.data();
+        ufc_data_frame_builder_add(&b, &d0);
+        ufc_data_frame_builder_add(&b, &d1);
+        const size_t fl2 = ufc_builder_build(&b, 1);
+        sendto(srv, out, fl2, 0, (sockaddr*)&from, fl);
+      }
+      served++;
+    }
+  });
+  const sockaddr_in to = loopback(a.port);
+  int ok = 0;
+  uint8_t buf[kFrame], out[kFrame];
+  for (int k = 0; k < kMsgs; k++) {
+    char msg[64];
+    snprintf(msg, sizeof(msg), "Hello world! #%d", k);  // echo_client.rs sends "Hello world!"
+    ufc_builder b;
+    ufc_data_frame_builder_init(&b, out, sizeof(out), (uint32_t)k, 0);
+    ufc_datagram_ref d{};
+    d.sequence_id = (uint32_t)k;
+    d.data = (const uint8_t*)msg;
+    d.data_len = strlen(msg);
+    ufc_data_frame_builder_add(&b, &d);
+    const size_t fl = ufc_builder_build(&b, 1);
+    sendto(cli, out, fl, 0, (const sockaddr*)&to, sizeof(to));
+    const ssize_t n = recv(cli, buf, sizeof(buf), 0);
+    ufc_frame_info info;
+    ufc_item items[4];
+    if (n > 0 && ufc_frame_read(buf, (size_t)n, &info, items, 4) == 1 && info.item_count == 2) {
+      std::string e0((const char*)buf + items[0].data_offset, items[0].data_len);
+      std::string e1((const char*)buf + items[1].data_offset, items[1].data_len);
+      std::string want(msg), rev(want.rbegin(), want.rend());
+      printf("[client] received \"%s\" / \"%s\"\n", e0.c_str(), e1.c_str());
+      if (e0 == want && e1 == rev && items[0].channel_id == 0 && items[1].channel_id == 1) ok++;
+    }
+  }
+  server.join();
+  close(srv);
+  close(cli);
+  printf("{\"config\": \"1: echo_client + echo_server over loopback, CPU CRC gate (frame plumbing)\", "
+         "\"messages\": %d, \"echoes_ok\": %d, \"served\": %d}\n",
+         kMsgs, ok, served.load());
+  return ok == kMsgs ? 0 : 1;
+}
+
+// ---------------- config 5: saturation with the gate in the receive path ----------------
+struct Batch {
+  uint8_t* slots = nullptr;  // batch * kFrame bytes (pinned when the gate is on the GPU)
+  std::vector<uint32_t> lens;
+  std::vector<uint32_t> crc;
+  std::vector<uint8_t> valid;
+  size_t n = 0;
+};
+
+int run_stream(const Args& a) {
+  ufc_ctx* ctx = nullptr;
+  if (a.gpu) {
+    const int rc = ufc_ctx_create(&ctx, 0);
+    if (rc != UFC_OK) {
+      fprintf(stderr, "ufc_ctx_create: %s\n", ufc_error_string(rc));
+      return 2;
+    }
+  }
+  const int rx = udp_socket(a.port, true, 256 << 20);
+  set_timeout(rx, 300);
+  const int tx = udp_socket(0, false, 0);
+  const size_t B = (size_t)a.batch;
+  // Sender: frames are built once (a ring of distinct frames, re-sent by sequence number).
+  const uint32_t kRing = 8192;
+  std::vector<uint8_t> ring((size_t)kRing * kFrame);
+  for (uint32_t s = 0; s < kRing; s++) build_stream_frame(ring.data() + (size_t)s * kFrame, s, true);
+  std::atomic<bool> sender_done{false};
+  std::atomic<uint64_t> sent{0};
+  std::thread sender([&] {
+    const sockaddr_in to = loopback(a.port);
+    const int M = 64;
+    std::vector<mmsghdr> msgs(M);
+    std::vector<iovec> iov(M);
+    std::vector<uint8_t> scratch((size_t)M * kFrame);
+    uint64_t s = 0;
+    while (s < a.frames) {
+      const int m = (int)std::min<uint64_t>(M, a.frames - s);
+      for (int i = 0; i < m; i++) {
+        const uint64_t q = s + i;
+        uint8_t* f = ring.data() + (size_t)(q % kRing) * kFrame;
+        if (a.corrupt_every && q % a.corrupt_every == a.corrupt_every - 1) {  // one flipped bit
+          memcpy(scratch.data() + (size_t)i * kFrame, f, kFrame);
+          f = scratch.data() + (size_t)i * kFrame;
+          f[100 + q % 1000] ^= 0x10;
+        }
+        iov[i].iov_base = f;
+        iov[i].iov_len = kFrame;
+        msgs[i].msg_hdr = msghdr{};
+        msgs[i].msg_hdr.msg_name = (void*)&to;
+        msgs[i].msg_hdr.msg_namelen = sizeof(to);
+        msgs[i].msg_hdr.msg_iov = &iov[i];
+        msgs[i].msg_hdr.msg_iovlen = 1;
+      }
+      const int r = sendmmsg(tx, msgs.data(), m, 0);
+      if (r > 0) s += r;
+    }
+    sent = s;
+    sender_done = true;
+  });
+  // Two batches: the receiver fills one while the worker gates and parses the other.
+  Batch bufs[2];
+  for (Batch& b : bufs) {
+    if (a.gpu) {
+      if (hipHostMalloc((void**)&b.slots, B * kFrame, hipHostMallocDefault) != hipSuccess) return 2;
+    } else {
+      b.slots = (uint8_t*)malloc(B * kFrame);
+    }
+    b.lens.resize(B);
+    b.crc.resize(B);
+    b.valid.resize(B);
+  }
+  std::mutex mu;
+  std::condition_variable cv;
+  int full = -1;           // index of the batch waiting for the worker
+  bool free_slot[2] = {true, true};
+  bool stop = false;
+  uint64_t n_valid = 0, n_invalid = 0, n_parsed = 0, n_payload_bad = 0, bytes_in = 0;
+  double t_gate = 0;
+  std::thread worker([&] {
+    std::vector<ufc_item> items(UFC_DATA_FRAME_MAX_DATAGRAM_COUNT);
+    std::vector<uint8_t> expect(kFragment);
+    for (;;) {
+      int k;
+      {
+        std::unique_lock<std::mutex> l(mu);
+        cv.wait(l, [&] { return full >= 0 || stop; });
+        if (full < 0 && stop) return;
+        k = full;
+        full = -1;
+      }
+      Batch& b = bufs[k];
+      const double t0 = now_s();
+      if (a.gpu) {
+        if (ufc_validate_host_slots(ctx, b.slots, kFrame, b.lens.data(), b.n, b.crc.data(), b.valid.data()) != UFC_OK)
+          abort();
+      } else {
+        for (size_t i = 0; i < b.n; i++) b.valid[i] = (uint8_t)ufc_frame_validate(b.slots + i * kFrame, b.lens[i]);
+      }
+      t_gate += now_s() - t0;
+      for (size_t i = 0; i < b.n; i++) {
+        const uint8_t* f = b.slots + i * kFrame;
+        bytes_in += b.lens[i];
+        if (!b.valid[i]) {
+          n_invalid++;
+          continue;
+        }
+        n_valid++;
+        ufc_frame_info info;
+        if (ufc_frame_parse(f, b.lens[i], 1, &info, items.data(), items.size()) != 1) continue;
+        n_parsed++;
+        if (a.verify && info.kind == UFC_FRAME_DATA && info.item_count == 1) {
+          const uint32_t seq = info.f[0], c = seq % kChannels, p = seq / kChannels;
+          if (items[0].channel_id != c || items[0].id != (p & 0xFFFFF) || items[0].data_len != kFragment) {
+            n_payload_bad++;
+            continue;
+          }
+          for (size_t j = 0; j < kFragment; j++) expect[j] = payload_byte(c, p, j);
+          if (memcmp(f + items[0].data_offset, expect.data(), kFragment) != 0) n_payload_bad++;
+        }
+      }
+      std::lock_guard<std::mutex> l(mu);
+      free_slot[k] = true;
+      cv.notify_all();
+    }
+  });
+  uint64_t received = 0;
+  double t_first = 0, t_last = 0;
+  std::vector<mmsghdr> msgs(B);
+  std::vector<iovec> iov(B);
+  int cur = 0;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> l(mu);
+      cv.wait(l, [&] { return free_slot[cur]; });
+      free_slot[cur] = false;
+    }
+    Batch& b = bufs[cur];
+    b.n = 0;
+    bool idle = false;
+    while (b.n < B) {
+      const size_t want = B - b.n;
+      for (size_t i = 0; i < want; i++) {
+        iov[i].iov_base = b.slots + (b.n + i) * kFrame;
+        iov[i].iov_len = kFrame;
+        msgs[i].msg_hdr = msghdr{};
+        msgs[i].msg_hdr.msg_iov = &iov[i];
+        msgs[i].msg_hdr.msg_iovlen = 1;
+      }
+      const int r = recvmmsg(rx, msgs.data(), (unsigned)want, MSG_WAITFORONE, nullptr);
+      if (r <= 0) {  // 300 ms without a datagram: the stream is over
+        idle = sender_done.load();
+        if (idle || received == 0) {
+          if (idle) break;
+          continue;
+        }
+        break;
+      }
+      if (received == 0) t_first = now_s();
+      for (int i = 0; i < r; i++) b.lens[b.n + i] = msgs[i].msg_len;
+      b.n += (size_t)r;
+      received += (uint64_t)r;
+      t_last = now_s();
+    }
+    {
+      std::unique_lock<std::mutex> l(mu);
+      if (b.n) {
+        cv.wait(l, [&] { return full < 0; });
+        full = cur;
+      } else {
+        free_slot[cur] = true;
+      }
+      cv.notify_all();
+    }
+    cur ^= 1;
+    if (idle) break;
+  }
+  {
+    std::unique_lock<std::mutex> l(mu);
+    cv.wait(l, [&] { return full < 0 && free_slot[0] && free_slot[1]; });
+    stop = true;
+    cv.notify_all();
+  }
+  worker.join();
+  sender.join();
+  const double secs = now_s() - t_first;
+  const double span = std::max(t_last - t_first, 1e-9);
+  printf("{\"config\": \"5: ideal_transfer-style loopback at saturation, %s CRC gate in the receive path\", "
+         "\"frame_bytes\": %zu, \"sent\": %llu, \"received\": %llu, \"valid\": %llu, \"invalid\": %llu, "
+         "\"parsed\": %llu, \"payload_mismatch\": %llu, \"receive_seconds\": %.4f, \"frames_per_s\": %.0f, "
+         "\"GB_s\": %.3f, \"gate_seconds\": %.4f, \"gate_GB_s\": %.3f, \"batch\": %d, \"total_seconds\": %.4f}\n",
+         a.gpu ? "GPU (ufc_validate_host_slots: H2D + kernel + D2H)" : "CPU (ufc_frame_validate, 1 thread)", kFrame,
+         (unsigned long long)sent.load(), (unsigned long long)received, (unsigned long long)n_valid,
+         (unsigned long long)n_invalid, (unsigned long long)n_parsed, (unsigned long long)n_payload_bad, span,
+         received / span, bytes_in / span / 1e9, t_gate, t_gate > 0 ? bytes_in / t_gate / 1e9 : 0.0, a.batch, secs);
+  for (Batch& b : bufs) {
+    if (a.gpu)
+      (void)hipHostFree(b.slots);
+    else
+      free(b.slots);
+  }
+  close(rx);
+  close(tx);
+  if (ctx) ufc_ctx_destroy(ctx);
+  return (n_payload_bad == 0 && received > 0) ? 0 : 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Args a;
+  for (int i = 1; i < argc; i++) {
+    const std::string s = argv[i];
+    auto next = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
+    if (s == "--echo") a.echo = true;
+    else if (s == "--gate") a.gpu = std::string(next()) != "cpu";
+    else if (s == "--frames") a.frames = strtoull(next(), nullptr, 10);
+    else if (s == "--batch") a.batch = atoi(next());
+    else if (s == "--port") a.port = (uint16_t)atoi(next());
+    else if (s == "--corrupt-every") a.corrupt_every = strtoull(next(), nullptr, 10);
+    else if (s == "--no-verify") a.verify = false;
+    else {
+      fprintf(stderr, "usage: %s [--echo] [--gate gpu|cpu] [--frames N] [--batch B] [--port P] "
+                      "[--corrupt-every K] [--no-verify]\n", argv[0]);
+      return 2;
+    }
+  }
+  return a.echo ? run_echo(a) : run_stream(a);
+}

@@ -48,6 +48,25 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
     return target
 
 
+LOOPBACK_SRC = os.path.join(REPO_DIR, "tools", "loopback", "ufc_loopback.cpp")
+LOOPBACK_BIN = os.path.join(REPO_DIR, "tools", "loopback", "ufc_loopback")
+
+
+def build_tools(force=False, verbose=False):
+    """The loopback harness (BASELINE.json configs 1 and 5), linked against the in-tree library."""
+    deps = [LOOPBACK_SRC, LIB_PATH] + [os.path.join(REPO_DIR, "include", h)
+                                        for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
+    if not force and not _stale(LOOPBACK_BIN, deps):
+        return LOOPBACK_BIN
+    cmd = [HIPCC, "-O2", "-std=c++17", "-Wall", "-o", LOOPBACK_BIN + ".tmp", LOOPBACK_SRC,
+           "-L" + PKG_DIR, "-luflowcrc", "-Wl,-rpath,$ORIGIN/../../uflow_amd", "-lpthread"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(LOOPBACK_BIN + ".tmp", LOOPBACK_BIN)
+    return LOOPBACK_BIN
+
+
 def build_oracle(force=False):
     odir = os.path.join(REPO_DIR, "oracle")
     target = os.path.join(odir, "liboracle.so")
@@ -60,4 +79,5 @@ def build_oracle(force=False):
 if __name__ == "__main__":
     build_native(force="--force" in sys.argv, verbose=True)
     build_oracle(force="--force" in sys.argv)
+    build_tools(force="--force" in sys.argv, verbose=True)
     print(LIB_PATH)

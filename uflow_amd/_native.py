@@ -48,6 +48,8 @@ _SIGNATURES = {
     # include/uflow_frame_codec.h
     "ufc_frame_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_size_t]),
+    "ufc_frame_parse": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_size_t]),
     "ufc_frame_write_fixed": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]),
     "ufc_data_frame_builder_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
                                                    ctypes.c_int]),

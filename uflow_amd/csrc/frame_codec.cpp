@@ -54,6 +54,17 @@ int ufc_frame_read(const uint8_t* frame, size_t len, ufc_frame_info* info, ufc_i
   return ok ? 1 : 0;
 }
 
+int ufc_frame_parse(const uint8_t* frame, size_t len, int crc_ok, ufc_frame_info* info, ufc_item* items,
+                    size_t items_cap) {
+  if (!info || (!frame && len)) return UFC_ERR_INVALID_ARG;
+  if (len > 0xFFFFFFFFu) len = 0xFFFFFFFFu;
+  const bool ok = ufc_codec::read_frame(HostBytes{frame}, (uint32_t)len, crc_ok != 0 && frame, *info, items,
+                                        (uint32_t)std::min<size_t>(items_cap, 0xFFFFFFFFu));
+  info->item_first = 0;
+  if (ok && info->item_count > items_cap && items) return UFC_ERR_NOMEM;
+  return ok ? 1 : 0;
+}
+
 size_t ufc_frame_write_fixed(const ufc_frame_info* info, uint8_t* out, size_t cap, int seal) {
   if (!info || !out) return 0;
   size_t len;
