@@ -16,6 +16,8 @@
  *   ufc_validate_host_varlen  the same gate for frames that start and end in host memory
  *   ufc_validate_host_slots   (a UDP receive buffer): H2D copy + GPU CRC + D2H copy; _slots takes the
  *                             recvmmsg layout (fixed-size slots + lengths) of the receive loops
+ *   ufc_seal_host_slots /     a flush's frames sealed in one batch before sendmmsg (the builders'
+ *   ufc_seal_host_varlen      build(), build.rs:151-159, for every frame of half_connection/emit.rs)
  *
  * Conventions (mirroring the reference):
  *   - All buffers are caller-owned; nothing is retained after a call returns (device calls:
@@ -101,6 +103,12 @@ int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_
  * no host-side compaction. */
 int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
                             size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out);
+/* The send side (a flush's frames laid out by the builders with zero trailers):
+ * CRC of every frame on the GPU (H2D of the frames, D2H of 4 B per frame), then the BE32 trailers
+ * are written into the host buffer.  h_crc_scratch: n words (receives the CRCs).  Lengths >= 4. */
+int ufc_seal_host_slots(ufc_ctx* ctx, uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens, size_t n,
+                        uint32_t* h_crc_scratch);
+int ufc_seal_host_varlen(ufc_ctx* ctx, uint8_t* h_bytes, const uint64_t* h_offsets, size_t n, uint32_t* h_crc_scratch);
 
 #ifdef __cplusplus
 }

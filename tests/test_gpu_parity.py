@@ -339,3 +339,24 @@ def test_host_slots(engine):
     assert np.array_equal(valid[::7], np.array([int(v) for v, _ in ref], np.uint8))
     assert np.array_equal(crc[::7], np.array([c for _, c in ref], np.uint32))
     assert int(valid.sum()) == n - len(range(0, n, 101))
+
+
+def test_seal_host_varlen(engine):
+    """Send-side batch seal of builder output (zero trailers) in host memory == per-frame seal."""
+    from uflow_amd.frame import DataFrameBuilder, Datagram
+    rng = np.random.default_rng(71)
+    frames = []
+    for i in range(5000):
+        b = DataFrameBuilder(i, bool(i & 1))
+        for k in range(int(rng.integers(0, 4))):
+            b.add(Datagram(int(rng.integers(0, 1 << 20)), int(rng.integers(0, 64)), int(rng.integers(0, 300)),
+                           int(rng.integers(0, 300)), 0, 0, bytes(rng.integers(0, 256, int(rng.integers(0, 400)),
+                                                                                dtype=np.uint8))))
+        frames.append(b.build(seal=False))
+    offsets = np.zeros(len(frames) + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum([len(f) for f in frames])
+    data = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
+    ref = data.copy()
+    oracle.seal_varlen(ref, offsets)
+    engine.seal_host_varlen(data, offsets)
+    assert np.array_equal(data, ref)

@@ -13,6 +13,9 @@
 //                 (ufc_validate_host_slots: H2D + kernel + D2H) or on the CPU (--gate cpu) -- then
 //                 the rest of Frame::read (ufc_frame_parse) and checks every payload byte.  The
 //                 reference does one recv_from + Frame::read per datagram (server/mod.rs:591-602).
+//                 --send-seal cpu|gpu: the sender builds every flush's frames with zero trailers and
+//                 seals them in one batch (per frame on the CPU, or ufc_seal_host_slots on the GPU)
+//                 before sendmmsg, the batched form of emit.rs:114-125 + build.rs:151-159.
 // Output: one JSON line (frames/s and GB/s of frame bytes received, gated and parsed).
 #include <arpa/inet.h>
 #include <hip/hip_runtime.h>
@@ -110,6 +113,7 @@ struct Args {
   uint16_t port = 8888;
   uint64_t corrupt_every = 0;  // flip one bit in every k-th frame (must be rejected)
   bool verify = true;
+  int send_seal = 0;  // 0: frames built once and re-sent; 1: built per flush, sealed on the CPU; 2: ... on the GPU
 };
 
 // ---------------- config 1: echo plumbing ----------------
@@ -218,8 +222,75 @@ int run_stream(const Args& a) {
   for (uint32_t s = 0; s < kRing; s++) build_stream_frame(ring.data() + (size_t)s * kFrame, s, true);
   std::atomic<bool> sender_done{false};
   std::atomic<uint64_t> sent{0};
+  // Send-side seal modes: every flush of F frames is laid out by the
+  // builder with zero trailers (payloads copied from a pool), sealed in one batch -- per frame on
+  // the CPU (ufc_frame_seal) or on the GPU (ufc_seal_host_slots) -- then sent with sendmmsg.
+  double t_send_seal = 0, t_send_total = 0;
+  ufc_ctx* sctx = nullptr;
+  if (a.send_seal == 2 && ufc_ctx_create(&sctx, 0) != UFC_OK) return 2;
   std::thread sender([&] {
     const sockaddr_in to = loopback(a.port);
+    const double t0 = now_s();
+    if (a.send_seal) {
+      const size_t F = 4096;
+      uint8_t* slab = nullptr;
+      if (sctx) {
+        if (hipHostMalloc((void**)&slab, F * kFrame, hipHostMallocDefault) != hipSuccess) abort();
+      } else {
+        slab = (uint8_t*)malloc(F * kFrame);
+      }
+      std::vector<uint32_t> lens(F), crcs(F);
+      std::vector<mmsghdr> msgs(F);
+      std::vector<iovec> iov(F);
+      uint64_t s = 0;
+      while (s < a.frames) {
+        const size_t m = (size_t)std::min<uint64_t>(F, a.frames - s);
+        for (size_t i = 0; i < m; i++) {
+          const uint32_t seq = (uint32_t)((s + i) % kRing);
+          uint8_t* f = slab + i * kFrame;
+          ufc_builder b;  // DataFrameBuilder::new + add (payload from the pool) with a zero trailer
+          ufc_data_frame_builder_init(&b, f, kFrame, seq, 0);
+          ufc_datagram_ref d{};
+          d.sequence_id = (seq / kChannels) & 0xFFFFF;
+          d.channel_id = (uint8_t)(seq % kChannels);
+          d.data = ring.data() + (size_t)seq * kFrame + 20;  // pool payload (6-B frame + 14-B datagram header)
+          d.data_len = kFragment;
+          ufc_data_frame_builder_add(&b, &d);
+          lens[i] = (uint32_t)ufc_builder_build(&b, 0);
+        }
+        const double ts = now_s();
+        if (sctx) {
+          if (ufc_seal_host_slots(sctx, slab, kFrame, lens.data(), m, crcs.data()) != UFC_OK) abort();
+        } else {
+          for (size_t i = 0; i < m; i++) ufc_frame_seal(slab + i * kFrame, lens[i]);
+        }
+        t_send_seal += now_s() - ts;
+        for (size_t i = 0; i < m; i++) {
+          const uint64_t q = s + i;
+          if (a.corrupt_every && q % a.corrupt_every == a.corrupt_every - 1) slab[i * kFrame + 100 + q % 1000] ^= 0x10;
+          iov[i].iov_base = slab + i * kFrame;
+          iov[i].iov_len = lens[i];
+          msgs[i].msg_hdr = msghdr{};
+          msgs[i].msg_hdr.msg_name = (void*)&to;
+          msgs[i].msg_hdr.msg_namelen = sizeof(to);
+          msgs[i].msg_hdr.msg_iov = &iov[i];
+          msgs[i].msg_hdr.msg_iovlen = 1;
+        }
+        for (size_t done = 0; done < m;) {
+          const int r = sendmmsg(tx, msgs.data() + done, (unsigned)std::min<size_t>(64, m - done), 0);
+          if (r > 0) done += (size_t)r;
+        }
+        s += m;
+      }
+      if (sctx)
+        (void)hipHostFree(slab);
+      else
+        free(slab);
+      t_send_total = now_s() - t0;
+      sent = s;
+      sender_done = true;
+      return;
+    }
     const int M = 64;
     std::vector<mmsghdr> msgs(M);
     std::vector<iovec> iov(M);
@@ -379,11 +450,15 @@ int run_stream(const Args& a) {
   printf("{\"config\": \"5: ideal_transfer-style loopback at saturation, %s CRC gate in the receive path\", "
          "\"frame_bytes\": %zu, \"sent\": %llu, \"received\": %llu, \"valid\": %llu, \"invalid\": %llu, "
          "\"parsed\": %llu, \"payload_mismatch\": %llu, \"receive_seconds\": %.4f, \"frames_per_s\": %.0f, "
-         "\"GB_s\": %.3f, \"gate_seconds\": %.4f, \"gate_GB_s\": %.3f, \"batch\": %d, \"total_seconds\": %.4f}\n",
+         "\"GB_s\": %.3f, \"gate_seconds\": %.4f, \"gate_GB_s\": %.3f, \"batch\": %d, \"total_seconds\": %.4f, "
+         "\"send_seal\": \"%s\", \"send_seal_seconds\": %.4f, \"send_seal_GB_s\": %.3f, \"send_seconds\": %.4f}\n",
          a.gpu ? "GPU (ufc_validate_host_slots: H2D + kernel + D2H)" : "CPU (ufc_frame_validate, 1 thread)", kFrame,
          (unsigned long long)sent.load(), (unsigned long long)received, (unsigned long long)n_valid,
          (unsigned long long)n_invalid, (unsigned long long)n_parsed, (unsigned long long)n_payload_bad, span,
-         received / span, bytes_in / span / 1e9, t_gate, t_gate > 0 ? bytes_in / t_gate / 1e9 : 0.0, a.batch, secs);
+         received / span, bytes_in / span / 1e9, t_gate, t_gate > 0 ? bytes_in / t_gate / 1e9 : 0.0, a.batch, secs,
+         a.send_seal == 0 ? "none (prebuilt frames)" : a.send_seal == 1 ? "cpu (ufc_frame_seal per frame)"
+                                                                       : "gpu (ufc_seal_host_slots per flush)",
+         t_send_seal, t_send_seal > 0 ? (double)sent.load() * kFrame / t_send_seal / 1e9 : 0.0, t_send_total);
   for (Batch& b : bufs) {
     if (a.gpu)
       (void)hipHostFree(b.slots);
@@ -393,6 +468,7 @@ int run_stream(const Args& a) {
   close(rx);
   close(tx);
   if (ctx) ufc_ctx_destroy(ctx);
+  if (sctx) ufc_ctx_destroy(sctx);
   return (n_payload_bad == 0 && received > 0) ? 0 : 1;
 }
 
@@ -410,9 +486,13 @@ int main(int argc, char** argv) {
     else if (s == "--port") a.port = (uint16_t)atoi(next());
     else if (s == "--corrupt-every") a.corrupt_every = strtoull(next(), nullptr, 10);
     else if (s == "--no-verify") a.verify = false;
+    else if (s == "--send-seal") {
+      const std::string v = next();
+      a.send_seal = v == "gpu" ? 2 : v == "cpu" ? 1 : 0;
+    }
     else {
       fprintf(stderr, "usage: %s [--echo] [--gate gpu|cpu] [--frames N] [--batch B] [--port P] "
-                      "[--corrupt-every K] [--no-verify]\n", argv[0]);
+                      "[--corrupt-every K] [--no-verify] [--send-seal none|cpu|gpu]\n", argv[0]);
       return 2;
     }
   }

@@ -138,6 +138,15 @@ class FrameCrcEngine:
         return infos, items, used
 
     # ---- host buffers (frames received into host memory) ----
+    def seal_host_varlen(self, data: np.ndarray, offsets: np.ndarray):
+        """Seal every frame of a host CSR batch in place (GPU CRC, host trailer write); returns the CRCs."""
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        n = offsets.size - 1
+        crc = np.empty(max(n, 0), dtype=np.uint32)
+        check(lib().ufc_seal_host_varlen(self._ctx, data.ctypes.data, offsets.ctypes.data, n, crc.ctypes.data),
+              "ufc_seal_host_varlen")
+        return crc
+
     def validate_host_slots(self, slots: np.ndarray, slot_stride: int, lens: np.ndarray):
         """Datagrams received into fixed-size slots (recvmmsg layout) -> (crc uint32[n], valid uint8[n])."""
         slots = np.ascontiguousarray(slots, dtype=np.uint8)

@@ -602,6 +602,39 @@ int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_st
   return UFC_OK;
 }
 
+namespace {
+void put_trailer(uint8_t* f, size_t len, uint32_t crc) {  // serial/mod.rs:466-470
+  uint8_t* t = f + len - 4;
+  t[0] = (uint8_t)(crc >> 24);
+  t[1] = (uint8_t)(crc >> 16);
+  t[2] = (uint8_t)(crc >> 8);
+  t[3] = (uint8_t)crc;
+}
+}  // namespace
+
+int ufc_seal_host_slots(ufc_ctx* ctx, uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens, size_t n,
+                        uint32_t* h_crc_scratch) {
+  if (!ctx || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (h_lens[i] < 4) return UFC_ERR_INVALID_ARG;
+  // The gate computes crc = compute(frame[..len-4]) whatever the trailer holds: that is the seal.
+  const int rc = ufc_validate_host_slots(ctx, h_slots, slot_stride, h_lens, n, h_crc_scratch, nullptr);
+  if (rc != UFC_OK) return rc;
+  for (size_t i = 0; i < n; i++) put_trailer(h_slots + i * slot_stride, h_lens[i], h_crc_scratch[i]);
+  return UFC_OK;
+}
+
+int ufc_seal_host_varlen(ufc_ctx* ctx, uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
+                         uint32_t* h_crc_scratch) {
+  if (!ctx || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (h_offsets[i + 1] < h_offsets[i] + 4) return UFC_ERR_INVALID_ARG;
+  const int rc = ufc_validate_host_varlen(ctx, h_bytes, h_offsets, n, h_crc_scratch, nullptr);
+  if (rc != UFC_OK) return rc;
+  for (size_t i = 0; i < n; i++) put_trailer(h_bytes + h_offsets[i], (size_t)(h_offsets[i + 1] - h_offsets[i]), h_crc_scratch[i]);
+  return UFC_OK;
+}
+
 int ufc_parse_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
                            const uint8_t* d_valid, ufc_frame_info* d_infos, ufc_item* d_items, size_t items_cap,
                            uint64_t* d_items_used, void* stream) {
