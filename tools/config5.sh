@@ -12,4 +12,9 @@ for gate in cpu gpu; do
       >> gpurun_out/config5.jsonl 2> gpurun_out/config5_$gate.err || { echo "$gate failed"; tail -3 gpurun_out/config5_$gate.err; exit 1; }
   done
 done
+# Send side too: every flush built with zero trailers and batch-sealed (CPU per frame, or GPU).
+for seal in cpu gpu; do
+  timeout -k 10 120 $B --gate gpu --send-seal $seal --frames ${FRAMES:-3000000} --port 18803 --corrupt-every 1000 \
+    >> gpurun_out/config5.jsonl 2> gpurun_out/config5_seal_$seal.err || { echo "seal $seal failed"; tail -3 gpurun_out/config5_seal_$seal.err; exit 1; }
+done
 cat gpurun_out/config5.jsonl
