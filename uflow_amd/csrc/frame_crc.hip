@@ -357,14 +357,20 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 // workgroup to finish resets both, so every launch finds them zero (launches of one slot are
 // stream-ordered; see ufc_api.cpp).
 
-template <int J, bool SEAL, int DEPTH, int ABL, bool DYN>
-__global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParams p) {
+template <int J, bool SEAL, int DEPTH, int ABL_, int SCHED, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const KernelParams p) {
   static_assert(DEPTH == 2 || DEPTH == 3, "pipeline depth (4 spills at J = 6)");
+  // Tuning ablation 5: loads only without the per-set finish.
+  constexpr bool NO_FINISH = ABL_ == 5;
+  constexpr int ABL = NO_FINISH ? kLeanAblLoads : ABL_;
+  constexpr bool DYN = SCHED == kSchedClaim;        // claimed sets (per-workgroup counter)
+  constexpr bool ILV = SCHED == kSchedInterleave;   // static: wave i takes lo + i + k * WAVES
+  constexpr uint32_t kInc = ILV ? (uint32_t)WAVES : 1u;  // step of a static sequence
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
 #ifdef UFC_TUNING
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-  const StageRegs sr = stage_load(p);
+  const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
   Lane L;
   init_lane(L, lds, p.G);
 
@@ -373,23 +379,31 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
   const uint32_t n = len - 4u;
   const int pad = J * 256 - (int)len;          // E = len
   const uint32_t nsets = (uint32_t)((p.nframes + 3) >> 2);  // < 2^32 (host chunks launches)
-  const uint32_t wpb = blockDim.x >> 6;
+  // The main loop covers the full sets; a partial last set (nframes % 4 frames) is done by the
+  // grid's last wave after its loop.  The host guarantees a full set past the edge sets.
+  const uint32_t nfull = (uint32_t)(p.nframes >> 2);
+  const bool tail = (p.nframes & 3) != 0;
+  const uint32_t wpb = WAVES;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t w = blockIdx.x * wpb + wid;  // global wave index
   // Sets before s_fast have a frame whose pad region precedes the buffer: they take the slow path
   // (global wave 0, before its main loop).  front_ok: bytes before the batch are readable (a
   // later chunk of a larger batch), so there are none.  With E = len the fast loads of a frame end exactly at
   // its last byte, so no set at the end of the batch is unsafe.
-  const uint32_t s_fast =
+  const uint32_t s_edge =
       p.front_ok ? 0u : (uint32_t)min(((uint64_t)pad + 4 * stride - 1) / (4 * stride), (uint64_t)nsets);
-  const uint32_t nfast = nsets - s_fast;
+  // A single edge set (every stride >= 65 B) is loaded on the fast path instead, with clamped
+  // addresses and byte shifts (load_edge0 below), when the batch holds at least 16 bytes.
+  const bool edge0 = s_edge == 1 && (p.nframes - 1) * stride + len >= 16;
+  const uint32_t s_fast = edge0 ? 0u : s_edge;
+  const uint32_t nfast = nfull - s_fast;
   // This wave's set sequence q0 < q1 < q2 < ... (strictly increasing, so once one is past `q_end`
   // all later ones are).  Static: a balanced contiguous range per wave.  Dynamic: the workgroup
   // owns a contiguous range; wave i starts with sets lo+i (and lo+16+i at depth 3), then claims
   // the following ones with a per-workgroup counter, so the 16 waves finish together whatever the SIMD arbitration does
   // (oldest-wave-first arbitration otherwise finishes a CU's waves in four staggered groups).
   uint32_t q_lo, q_end, q_cur, q_nx1, q_nx2;
-  if (DYN) {
+  if (DYN || ILV) {
     q_lo = s_fast + (uint32_t)((uint64_t)nfast * blockIdx.x / gridDim.x);
     q_end = s_fast + (uint32_t)((uint64_t)nfast * (blockIdx.x + 1) / gridDim.x);
     q_cur = q_lo + wid;
@@ -472,7 +486,10 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
   };
   // Finish set q (this run's t-th): the trailer word (lane 15 of the frame's row) is broadcast to
   // the row (DPP row_newbcast:15), so every lane of the frame has its validity.
-  auto finish = [&](uint32_t q, const Chains& c) {
+  // may_overflow: more than 16 * kLeanRuns sets may reach this wave's history (claimed schedule,
+  // the tail set); the static schedules never overflow inside the loop (host chunking), so
+  // their loop carries no store path.
+  auto finish = [&](uint32_t q, const Chains& c, bool may_overflow) {
     const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
     const uint32_t ok = (len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
@@ -482,7 +499,7 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
       // shift the run into the history (hist[0] newest); a full history is stored first, followed
       // by an explicit vmcnt(0) so that no store stays pending into the loop (rare: > 128 sets
       // per wave in one launch).
-      if (nhist == kLeanRuns) {
+      if (may_overflow && nhist == kLeanRuns) {
         store_hist();
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
         nhist = 0;
@@ -530,18 +547,49 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
       }
     }
   };
-  // Lane load address of set q.  The last set may hold frames past nframes; those lanes re-read
-  // frame nframes-1 (loads never leave the buffer) and their results are not stored.  A set past
-  // the wave's range (prefetches of the final round, claims past the end) reads the nibble image
-  // instead: 32 KiB of valid, L2-resident memory, so it costs no HBM traffic.
-  auto lane_ptr = [&](uint32_t q) -> const uint8_t* {
-    const uint32_t qc = min(q, nsets - 1);
-    const uint32_t room = (uint32_t)(p.nframes - 1 - 4 * (uint64_t)qc);
-    const int64_t over = (int64_t)L.grp - (int64_t)min(room, 3u);
-    const uint8_t* a = p.bytes + (uint64_t)qc * 4 * stride + lane_off - (over > 0 ? over * (int64_t)stride : 0);
-    return q < q_end ? a : (const uint8_t*)p.nib_img + 16 * L.col;
+  // Loads of a main-loop set: a wave-uniform set base (SGPRs) plus this lane's loop-invariant
+  // 32-bit offset, so no per-set VGPR address arithmetic (whose registers the allocator may take
+  // from a pending load, stalling the next prefetch on the previous one).  A set past the range
+  // (the final prefetches) re-reads the last full set, which stays L2-resident.
+  const uint32_t voff = (uint32_t)(lane_off + 512);  // lane_off >= -259
+  auto set_base = [&](uint32_t q) -> const uint8_t* {
+    return p.bytes + (uint64_t)(q < q_end ? q : nfull - 1) * 4 * stride - 512;
   };
-  auto load = [&](uint32_t q, ItemBuf<J>& b) { load_set<J>(lane_ptr(q), b); };
+  // Set 0 when its first frames' pad bytes precede the buffer: pieces that start before the
+  // buffer load its first 16 bytes and shift them into place (the bytes before the buffer are
+  // pad, masked by the front fix); pieces wholly before it are zeros.  Prologue only.
+  auto load_edge0 = [&](ItemBuf<J>& b) {
+    const int64_t room = (int64_t)min(p.nframes - 1, (uint64_t)3);
+    const int64_t over = (int64_t)L.grp > room ? (int64_t)L.grp - room : 0;
+    const int64_t off0 = lane_off - over * (int64_t)stride;
+#pragma unroll
+    for (int j = 0; j < J; j++) {
+      const int64_t off = off0 + 256 * j;
+      uint4 v = load_frame16<true>(p.bytes + (off < 0 ? 0 : off));
+      if (off < 0) {
+        const int64_t d = -off;
+        uint64_t lo = (uint64_t)v.x | ((uint64_t)v.y << 32), hi = (uint64_t)v.z | ((uint64_t)v.w << 32);
+        if (d >= 16) {
+          lo = hi = 0;
+        } else if (d >= 8) {
+          hi = lo << (8 * (d - 8));
+          lo = 0;
+        } else {
+          hi = (hi << (8 * d)) | (lo >> (64 - 8 * d));
+          lo = lo << (8 * d);
+        }
+        v = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+      }
+      b.x[j] = v;
+    }
+  };
+  auto load = [&](uint32_t q, ItemBuf<J>& b) { load_set<J>(set_base(q), voff, b); };
+  // The partial last set: lanes of frames past nframes re-read frame nframes - 1.
+  auto load_tail = [&](ItemBuf<J>& b) {
+    const int64_t room = (int64_t)(p.nframes - 1 - 4 * (uint64_t)nfull);
+    const int64_t over = (int64_t)L.grp > room ? (int64_t)L.grp - room : 0;
+    load_set<J>(p.bytes + (uint64_t)nfull * 4 * stride - 512, voff - (uint32_t)(over * (int64_t)stride), b);
+  };
 
   // Prologue: claim (dynamic), first prefetches, then the LDS tables: HBM is busy from the start.
   // Depth 3 keeps q_cur and q_nx1 in flight and loads q_nx2 in the first step; depth 2 keeps
@@ -555,13 +603,16 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
     cY = claim_issue();
     cZ = claim_issue();
   }
-  load(q_cur, A);
+  if (edge0 && q_cur == 0)
+    load_edge0(A);
+  else
+    load(q_cur, A);
   if (DEPTH == 3) load(q_nx1, B);
-  stage_store(sr, lds);
+  stage_store<WAVES * 64>(sr, lds);
 #ifdef UFC_TUNING
   const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
 #endif
-  q_nx2 = (DEPTH == 3 && !DYN) ? q_lo + 2 : 0;
+  q_nx2 = (DEPTH == 3 && !DYN) ? q_cur + 2 * kInc : 0;
 
   // Edge sets [0, s_fast) (the first sets of the batch only): global wave 0, before its main
   // loop (the dynamic schedule rebalances), byte loads restricted to the frame, results stored
@@ -618,22 +669,30 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
     __builtin_amdgcn_sched_barrier(0);
     if (q_cur < q_end) {
       compute(q_cur, cur, c);
-      finish(q_cur, c);
+      if (NO_FINISH)
+        acc_crc ^= c.v0 ^ c.v1 ^ c.v2 ^ c.v3;
+      else
+        finish(q_cur, c, DYN);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (DEPTH == 3) {
       q_cur = q_nx1;
       q_nx1 = q_load;
-      q_nx2 = q_load + 1;
+      q_nx2 = q_load + kInc;
     } else {
       q_cur = q_load;
-      q_nx1 = q_load + 1;
+      q_nx1 = q_load + kInc;
     }
   };
   // Whole rounds of DEPTH steps with one uniform trip test (no early exits inside a round: they
   // would merge into the loop latch and poison the wait counts at the loop header).  The claim
   // ring rotates with period 3: step j issues into ring[j % 3] and reads ring[(j + 1) % 3].
-  if (DEPTH == 2) {
+  if (DEPTH == 2 && !DYN) {  // static schedules: no claim ring, rounds of two steps
+    while (q_cur < q_end) {
+      step(A, B, cX, cY);
+      step(B, A, cY, cZ);
+    }
+  } else if (DEPTH == 2) {
     while (q_cur < q_end) {
       step(A, B, cX, cY);
       step(B, A, cY, cZ);
@@ -648,6 +707,16 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
       step(B, A, cY, cZ);
       step(C, B, cZ, cX);
     }
+  }
+  if (tail && blockIdx.x == gridDim.x - 1 && wid == wpb - 1) {  // the partial last set
+    ItemBuf<J> T;
+    load_tail(T);
+    compute(nfull, T, c);
+    finish(nfull, c, true);
+  }
+  if (NO_FINISH) {  // keep the folded loads alive (tuning ablation)
+    if (p.crc_out) p.crc_out[blockIdx.x * blockDim.x + threadIdx.x] = acc_crc;
+    return;
   }
   // Results: the partial run, then the history.
   if (t > 0) store_run((int)t, acc_crc, acc_qv);
@@ -676,41 +745,106 @@ __global__ __launch_bounds__(1024) void frame_crc_fixed_kernel(const KernelParam
 #endif
 }
 
-#define UFC_INST_FIXED(J)                                                                      \
-  template __global__ void frame_crc_fixed_kernel<J, false, 3, 0, true>(const KernelParams);   \
-  template __global__ void frame_crc_fixed_kernel<J, true, 3, 0, true>(const KernelParams);
+// Product configurations: the default (interleaved schedule, 8 waves, depth 2; measured fastest,
+// DESIGN.md section 5.1) and the claimed schedule at 16 waves / depth 3 (the previous default, kept
+// for A/B through UFC_LEAN_CFG=claim16).
+#define UFC_INST_FIXED(J)                                                                                  \
+  template __global__ void frame_crc_fixed_kernel<J, false, 2, 0, kSchedInterleave, 8>(const KernelParams); \
+  template __global__ void frame_crc_fixed_kernel<J, true, 2, 0, kSchedInterleave, 8>(const KernelParams);  \
+  template __global__ void frame_crc_fixed_kernel<J, false, 3, 0, kSchedClaim, 16>(const KernelParams);     \
+  template __global__ void frame_crc_fixed_kernel<J, true, 3, 0, kSchedClaim, 16>(const KernelParams);
 UFC_INST_FIXED(1) UFC_INST_FIXED(2) UFC_INST_FIXED(3) UFC_INST_FIXED(4) UFC_INST_FIXED(5) UFC_INST_FIXED(6)
 
 #ifdef UFC_TUNING
-// A/B variants (J = 6, validate): static schedule, depth 2, ablations.
-template __global__ void frame_crc_fixed_kernel<6, false, 3, 0, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 2, 0, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, true>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, false>(const KernelParams);
-template __global__ void frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, false>(const KernelParams);
+// Loads-only streaming probe over a fixed-length batch (tuning builds only): the lean kernel's
+// lane->address pattern (4 frames per wave-instruction, 256-B runs right-aligned to the frame end),
+// static interleaved schedule, NBUF sets in flight per wave, no LDS (STAGE: the lean kernel's LDS
+// table staging first).  Results are meaningless (an XOR fold per lane lands in crc_out).
+template <int NBUF, int WAVES, bool STAGE>
+__global__ __launch_bounds__(WAVES * 64) void fixed_probe_kernel(const KernelParams p) {
+  __shared__ __attribute__((aligned(16))) char lds[STAGE ? kLdsBytes : 16];
+  constexpr int NI = 6;
+  if (STAGE) {
+    const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
+    stage_store<WAVES * 64>(sr, lds);
+  }
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nsets = (int)(p.nframes / 4);
+  const int lo = (int)((int64_t)nsets * blockIdx.x / gridDim.x);
+  const int hi = (int)((int64_t)nsets * (blockIdx.x + 1) / gridDim.x);
+  const int64_t stride = (int64_t)p.stride;
+  uint32_t acc = 0;
+  uint4 buf[NBUF][NI];
+  auto load = [&](int q, uint4 (&x)[NI]) {
+    const int qc = min(q, nsets - 1);
+    const int f = lane >> 4, col = lane & 15;
+    int64_t off = (int64_t)qc * 4 * stride + f * stride + 16 * col - (NI * 256 - (int64_t)p.frame_len);
+    off = off < 0 ? 0 : off;
+#pragma unroll
+    for (int j = 0; j < NI; j++) {
+      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(p.bytes + off + 256 * j));
+      x[j] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  };
+  int q = lo + wid;
+#pragma unroll
+  for (int b = 0; b < NBUF - 1; b++) load(q + WAVES * b, buf[b]);
+  for (; q < hi; q += WAVES * NBUF) {
+#pragma unroll
+    for (int b = 0; b < NBUF; b++) {
+      load(q + WAVES * (b + NBUF - 1), buf[(b + NBUF - 1) % NBUF]);
+      if (q + WAVES * b < hi) {
+#pragma unroll
+        for (int j = 0; j < NI; j++) acc ^= buf[b][j].x ^ buf[b][j].y ^ buf[b][j].z ^ buf[b][j].w;
+      }
+    }
+  }
+  if (STAGE) acc ^= *(const uint32_t*)(lds + 4 * (threadIdx.x & 31));
+  if (p.crc_out) p.crc_out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
 #endif
 
-const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, bool dyn) {
-  if (abl == 0 && depth == 3 && dyn) {
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves) {
+  if (abl == 0 && ((depth == 2 && sched == kSchedInterleave && waves == 8) ||
+                   (depth == 3 && sched == kSchedClaim && waves == 16))) {
+    const bool ilv = sched == kSchedInterleave;
     switch (J) {
-#define UFC_PICK_FIXED(JJ) \
-  case JJ: return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0, true> : (const void*)frame_crc_fixed_kernel<JJ, false, 3, 0, true>;
+#define UFC_PICK_FIXED(JJ)                                                                          \
+  case JJ:                                                                                          \
+    if (ilv)                                                                                        \
+      return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 2, 0, kSchedInterleave, 8>        \
+                  : (const void*)frame_crc_fixed_kernel<JJ, false, 2, 0, kSchedInterleave, 8>;      \
+    return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0, kSchedClaim, 16>              \
+                : (const void*)frame_crc_fixed_kernel<JJ, false, 3, 0, kSchedClaim, 16>;
       UFC_PICK_FIXED(1) UFC_PICK_FIXED(2) UFC_PICK_FIXED(3) UFC_PICK_FIXED(4) UFC_PICK_FIXED(5) UFC_PICK_FIXED(6)
 #undef UFC_PICK_FIXED
       default: return nullptr;
     }
   }
 #ifdef UFC_TUNING
-  if (J == 6 && !seal) {
-    if (abl == 0 && depth == 3 && !dyn) return (const void*)frame_crc_fixed_kernel<6, false, 3, 0, false>;
-    if (abl == 0 && depth == 2 && dyn) return (const void*)frame_crc_fixed_kernel<6, false, 2, 0, true>;
-    if (depth == 3 && abl == kLeanAblLoads)
-      return dyn ? (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, true>
-                 : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblLoads, false>;
-    if (depth == 3 && abl == kLeanAblCompute)
-      return dyn ? (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, true>
-                 : (const void*)frame_crc_fixed_kernel<6, false, 3, kLeanAblCompute, false>;
+  if (J == 6 && !seal && abl >= 3 && abl <= 4 && (depth == 2 || depth == 3)) {  // loads-only probes
+    static const void* const ptab[2][2][2] = {  // [waves 8/16][stage][nbuf 2/3]
+        {{(const void*)fixed_probe_kernel<2, 8, false>, (const void*)fixed_probe_kernel<3, 8, false>},
+         {(const void*)fixed_probe_kernel<2, 8, true>, (const void*)fixed_probe_kernel<3, 8, true>}},
+        {{(const void*)fixed_probe_kernel<2, 16, false>, (const void*)fixed_probe_kernel<3, 16, false>},
+         {(const void*)fixed_probe_kernel<2, 16, true>, (const void*)fixed_probe_kernel<3, 16, true>}}};
+    return ptab[waves == 16][abl == 4][depth - 2];
+  }
+  if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedInterleave && abl == 5)
+    return (const void*)frame_crc_fixed_kernel<6, false, 2, 5, kSchedInterleave, 8>;
+  if (J == 6 && !seal && (depth == 2 || depth == 3) && abl >= 0 && abl <= 2 && sched >= 0 && sched <= 2) {
+    // A/B variants (J = 6, validate), instantiated by taking their addresses here.
+    static const void* const tab[2][3][3][2] = {  // [waves 8/16][sched][abl][depth 2/3]
+#define UFC_T(WV, SC, AB) {(const void*)frame_crc_fixed_kernel<6, false, 2, AB, SC, WV>, \
+                           (const void*)frame_crc_fixed_kernel<6, false, 3, AB, SC, WV>}
+#define UFC_TS(WV, SC) {UFC_T(WV, SC, 0), UFC_T(WV, SC, kLeanAblLoads), UFC_T(WV, SC, kLeanAblCompute)}
+#define UFC_TW(WV) {UFC_TS(WV, kSchedRange), UFC_TS(WV, kSchedClaim), UFC_TS(WV, kSchedInterleave)}
+        UFC_TW(8), UFC_TW(16)};
+#undef UFC_TW
+#undef UFC_TS
+#undef UFC_T
+    return tab[waves == 16][sched][abl][depth - 2];
   }
 #endif
   return nullptr;

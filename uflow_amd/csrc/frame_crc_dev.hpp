@@ -244,12 +244,6 @@ struct ItemBuf {
   uint4 x[JC];
 };
 
-#ifndef UFC_LEAN_NT
-// Cache policy of the frame loads: 1 = all non-temporal (streaming); 0 = all default;
-// 2 = default for the first and last block of a frame (their boundary lines are shared with the
-// neighbouring frames and re-read shortly after), non-temporal for the blocks in between.
-#define UFC_LEAN_NT 1
-#endif
 template <bool NT>
 __device__ __forceinline__ uint4 load_frame16(const uint8_t* q) {
   u32x4 v;
@@ -259,44 +253,68 @@ __device__ __forceinline__ uint4 load_frame16(const uint8_t* q) {
     v = *as_global<g_u32x4>(q);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
-// One set's J blocks for this lane (lane address q = block 0).
+// One set's J blocks for this lane: block j at sbase + voff + 256*j, as raw buffer loads on a
+// wave-uniform resource (base = sbase, in SGPRs) with this lane's loop-invariant 32-bit offset in
+// a VGPR: no per-set VGPR address arithmetic, whose registers the allocator may otherwise take
+// from a pending load (the next prefetch then waits for the previous one).
+constexpr uint32_t kFixRecords = 0x7FFFFFF0u;  // far above any lane offset (host-checked stride)
+constexpr int kFixRsrcWord3 = 0x00020000;      // gfx9-family raw buffer descriptor word 3
+constexpr int kFixAuxNT = 2;                   // cache policy of the frame loads: nt (streaming)
 template <int J>
-__device__ __forceinline__ void load_set(const uint8_t* q, ItemBuf<J>& b) {
-  constexpr bool kEdgeNT = UFC_LEAN_NT == 1, kMidNT = UFC_LEAN_NT != 0;
-  b.x[0] = load_frame16<kEdgeNT>(q);
+__device__ __forceinline__ void load_set(const uint8_t* sbase, uint32_t voff, ItemBuf<J>& b) {
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)sbase, 0, (int)kFixRecords, kFixRsrcWord3);
 #pragma unroll
-  for (int j = 1; j < J - 1; j++) b.x[j] = load_frame16<kMidNT>(q + 256 * j);
-  if constexpr (J > 1) b.x[J - 1] = load_frame16<kEdgeNT>(q + 256 * (J - 1));
+  for (int j = 0; j < J; j++) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(voff + 256u * j), 0, kFixAuxNT);
+    b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+  }
 }
 
 constexpr int kLeanAblLoads = 1;
 constexpr int kLeanAblCompute = 2;
 
+// The tables are staged as 1024 chunks (one chain-table word replicated 32x + 32 B of the nibble
+// image each); a workgroup of THREADS threads stages 1024 / THREADS chunks per thread.
 struct StageRegs {
   uint32_t cv;
   u32x4 n0, n1;
 };
+template <int THREADS = 1024>
+struct StageSet {
+  static_assert(1024 % THREADS == 0, "workgroup size must divide 1024");
+  StageRegs r[1024 / THREADS];
+};
 
-__device__ __forceinline__ StageRegs stage_load(const KernelParams& p) {
-  const int t = threadIdx.x;
-  StageRegs r;
-  r.cv = *as_global<g_u32>(p.chain_tab + t);
-  r.n0 = *as_global<g_u32x4>(p.nib_img + 8 * t);
-  r.n1 = *as_global<g_u32x4>(p.nib_img + 8 * t + 4);
-  return r;
+template <int THREADS = 1024>
+__device__ __forceinline__ StageSet<THREADS> stage_load(const KernelParams& p) {
+  StageSet<THREADS> s;
+#pragma unroll
+  for (int i = 0; i < 1024 / THREADS; i++) {
+    const int t = threadIdx.x + i * THREADS;
+    s.r[i].cv = *as_global<g_u32>(p.chain_tab + t);
+    s.r[i].n0 = *as_global<g_u32x4>(p.nib_img + 8 * t);
+    s.r[i].n1 = *as_global<g_u32x4>(p.nib_img + 8 * t + 4);
+  }
+  return s;
 }
 
 // LDS writes of the staged tables, then a workgroup barrier that orders LDS only: data
 // prefetches issued before it stay in flight (no vmcnt(0) at the barrier).
-__device__ __forceinline__ void stage_store(const StageRegs& r, char* lds) {
-  const int t = threadIdx.x;
-  const uint32_t k = (uint32_t)t >> 8, e = (uint32_t)t & 255u;
-  const uint32_t cbase = kChainBase + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
-  const u32x4 cr = {r.cv, r.cv, r.cv, r.cv};
+template <int THREADS = 1024>
+__device__ __forceinline__ void stage_store(const StageSet<THREADS>& s, char* lds) {
 #pragma unroll
-  for (int i = 0; i < 8; i++) *(u32x4*)(lds + cbase + 16 * i) = cr;
-  *(u32x4*)(lds + 32 * t) = r.n0;
-  *(u32x4*)(lds + 32 * t + 16) = r.n1;
+  for (int i = 0; i < 1024 / THREADS; i++) {
+    const int t = threadIdx.x + i * THREADS;
+    const StageRegs& r = s.r[i];
+    const uint32_t k = (uint32_t)t >> 8, e = (uint32_t)t & 255u;
+    const uint32_t cbase = kChainBase + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;
+    const u32x4 cr = {r.cv, r.cv, r.cv, r.cv};
+#pragma unroll
+    for (int j = 0; j < 8; j++) *(u32x4*)(lds + cbase + 16 * j) = cr;
+    *(u32x4*)(lds + 32 * t) = r.n0;
+    *(u32x4*)(lds + 32 * t + 16) = r.n1;
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");

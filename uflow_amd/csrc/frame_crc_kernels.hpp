@@ -35,14 +35,22 @@ struct KernelParams {
 const void* kernel_symbol(int jc, int mode);
 bool config_available(int jc);
 // Lean fixed-length kernel (frame_len >= 4, J = ceil((frame_len + 4) / 256) in 1..6); one
-// workgroup per CU owning a contiguous range of 4-frame sets, handed to its 16 waves dynamically
-// (dyn) or as static per-wave ranges (tuning A/B); `depth` (2 or 3) sets in flight per wave.
-// abl != 0 selects the ablation variants of tuning builds (J = 6 only).
-constexpr int kLeanDepthDefault = 3;
+// workgroup per CU owning a contiguous range of 4-frame sets, spread over its waves by `sched`;
+// `depth` (2 or 3) sets in flight per wave.  Product default: interleaved, 8 waves, depth 2.
+// abl != 0 selects the ablation variants and loads-only probes of tuning builds (J = 6 only).
+constexpr int kLeanDepthDefault = 2;
 // Results stay in registers until a wave's range is done: at most 16 * kLeanRuns sets per wave,
 // i.e. a launch covers at most (waves in the grid) * 16 * kLeanRuns * 4 frames (host-chunked).
 constexpr int kLeanRuns = 8;
-const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, bool dyn);
+// waves: 16 (1024-thread workgroups) or 8 (512); one workgroup per CU either way (160 KiB LDS).
+constexpr int kLeanWavesDefault = 8;
+// Schedules of a workgroup's contiguous set range over its waves: per-wave contiguous ranges,
+// claimed one set at a time from a per-workgroup counter, or interleaved (wave i: lo + i + k*waves).
+constexpr int kSchedRange = 0;
+constexpr int kSchedClaim = 1;
+constexpr int kSchedInterleave = 2;
+constexpr int kLeanSchedDefault = kSchedInterleave;
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves);
 // Lean variable-length kernel (CSR offsets, any frame lengths; frames of 4..1532 B on the fast
 // path, the rest byte-wise after the main loop).  Set indices are 30-bit: a launch covers fewer
 // than 2^32 frames (host-chunked).

@@ -98,7 +98,7 @@ constexpr int kAuxNT = 2;               // cache policy bits of the load: nt (st
 template <bool SEAL, bool PAIRS, int ABL>
 __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelParams p) {
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-  const StageRegs sr = stage_load(p);
+  const StageSet<1024> sr = stage_load<1024>(p);
   Lane L;
   init_lane(L, lds, p.G);
   constexpr int JM = kVlBlocks;

@@ -103,10 +103,15 @@ int launch(ufc_ctx* ctx, Config cfg, int mode, ufc_dev::KernelParams& kp, hipStr
 
 // Lean fixed-length kernel: J = blocks per frame when 4 <= frame_len and J <= 6, else 0.  The
 // generic kernel stays reachable with UFC_FIXED_KERNEL=generic (A/B measurement) or UFC_FIXED_JC.
-int lean_fixed_blocks(uint64_t frame_len) {
+// The batch must also hold a full 4-frame set past the edge sets (those whose first frames' pad
+// bytes precede the buffer), which the kernel's out-of-range prefetches re-read.
+int lean_fixed_blocks(uint64_t frame_len, uint64_t stride, uint64_t n) {
   if (frame_len < 4) return 0;
   const uint64_t J = (frame_len + 4 + 255) / 256;
-  if (J > 6) return 0;
+  if (J > 6 || stride >= (1ull << 28)) return 0;  // lane offsets (3 strides + 2 KiB) stay below 2^31
+  const uint64_t pad = 256 * J - frame_len;
+  const uint64_t s_edge = (pad + 4 * stride - 1) / (4 * stride);
+  if (n / 4 <= s_edge) return 0;
   const char* k = std::getenv("UFC_FIXED_KERNEL");
   if (k && std::strcmp(k, "generic") == 0) return 0;
   if (std::getenv("UFC_FIXED_JC")) return 0;
@@ -114,17 +119,27 @@ int lean_fixed_blocks(uint64_t frame_len) {
 }
 
 int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  int depth = ufc_dev::kLeanDepthDefault, abl = 0;
-  bool dyn = true;
+  int depth = ufc_dev::kLeanDepthDefault, abl = 0, waves = ufc_dev::kLeanWavesDefault;
+  int sched = ufc_dev::kLeanSchedDefault;
+  if (const char* cfg = std::getenv("UFC_LEAN_CFG")) {  // A/B: the previous default
+    if (std::strcmp(cfg, "claim16") == 0) {
+      depth = 3;
+      sched = ufc_dev::kSchedClaim;
+      waves = 16;
+    }
+  }
 #ifdef UFC_TUNING
   // A/B knobs of the validate path (tuning builds): pipeline depth, schedule, ablations.
   if (!seal) {
     if (const char* d = std::getenv("UFC_LEAN_DEPTH")) depth = std::atoi(d);
     if (const char* ab = std::getenv("UFC_LEAN_ABL")) abl = std::atoi(ab);
-    if (const char* dy = std::getenv("UFC_LEAN_DYN")) dyn = std::atoi(dy) != 0;
+    if (const char* sc = std::getenv("UFC_LEAN_SCHED")) sched = std::atoi(sc);
   }
 #endif
-  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl, dyn);
+#ifdef UFC_TUNING
+  if (const char* wv = std::getenv("UFC_LEAN_WAVES")) waves = std::atoi(wv);  // A/B: 8 or 16
+#endif
+  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl, sched, waves);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain;
   kp.nib_img = ctx->d_nib;
@@ -132,17 +147,24 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
   // One 1024-thread workgroup per CU.  A launch covers at most `chunk` frames (32-bit set
   // indices; a wave's results mostly stay in registers until the end); every frame of a chunk
   // keeps its absolute address, and chunks after the first may read the pad bytes before them.
-  const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
-  const uint64_t chunk = (uint64_t)ctx->ncu * waves_per_block * 16 * ufc_dev::kLeanRuns * 4;
+  const uint64_t waves_per_block = (uint64_t)waves;
+  // (16 * kLeanRuns - 1 sets per wave: the static schedules' histories never overflow in the loop)
+  const uint64_t chunk = (uint64_t)ctx->ncu * waves_per_block * (16 * ufc_dev::kLeanRuns - 1) * 4;
   const uint64_t total = kp.nframes;
-  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
+  for (uint64_t f0 = 0, step = 0; f0 < total; f0 += step) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
+    // Every launch needs a full set (see lean_fixed_blocks): never leave a final chunk of < 4 frames.
+    if (total - f0 - c.nframes > 0 && total - f0 - c.nframes < 4) c.nframes -= 4;
+    step = c.nframes;
     c.bytes = kp.bytes + f0 * kp.stride;
     if (kp.wbytes) c.wbytes = kp.wbytes + f0 * kp.stride;
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
     c.front_ok = f0 > 0 ? 1u : 0u;
+#ifdef UFC_TUNING
+    if (std::getenv("UFC_FRONT_OK")) c.front_ok = 1u;  // A/B only: the caller guarantees readable pad bytes
+#endif
     // Claim counters: one slot of the ring per launch (zero on entry, reset by the kernel).
     const uint32_t slot = ctx->ctr_seq.fetch_add(1) % kCtrSlots;
     c.ctr = ctx->d_ctr + (size_t)slot * ctx->ncu * ufc_dev::kCtrWordsPerBlock;
@@ -157,7 +179,7 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
     if (dbg_path && hipMalloc(&d_dbg, blocks * waves_per_block * 32) == hipSuccess) c.dbg = d_dbg;
 #endif
     void* args[] = {&c};
-    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
 #ifdef UFC_TUNING
     if (d_dbg) {
@@ -199,6 +221,8 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
   for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
+    // Every launch needs a full set (see lean_fixed_blocks): never leave a final chunk of < 4 frames.
+    if (total - f0 - c.nframes > 0 && total - f0 - c.nframes < 4) c.nframes -= 4;
     c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
@@ -348,7 +372,7 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
     return UFC_ERR_INVALID_ARG;
   int freeze;
   const Config cfg = fixed_config(frame_len, &freeze);
-  int lean = lean_fixed_blocks(frame_len);
+  int lean = lean_fixed_blocks(frame_len, stride, n);
 #ifdef UFC_TUNING
   if (const char* ab = std::getenv("UFC_ABLATE")) {
     freeze |= std::atoi(ab);
@@ -398,7 +422,8 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
-  if (const int lean = lean_fixed_blocks(frame_len)) return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
+  if (const int lean = lean_fixed_blocks(frame_len, stride, n))
+    return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
   return launch(ctx, cfg, freeze | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
 
