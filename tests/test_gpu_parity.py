@@ -360,3 +360,32 @@ def test_seal_host_varlen(engine):
     oracle.seal_varlen(ref, offsets)
     engine.seal_host_varlen(data, offsets)
     assert np.array_equal(data, ref)
+
+
+@pytest.mark.parametrize("frame_len,extra", [(64, 3), (1500, 1), (1472, 2)])
+def test_fixed_multi_launch(engine, frame_len, extra):
+    """Batches the host splits into several lean launches (8 waves x 127 sets x 4 frames per CU
+    each), with a remainder that would leave a final launch of < 4 frames: GPU seal, then GPU
+    validate -> every frame valid except planted flips; a sample bit-exact vs the oracle."""
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    chunk = ncu * 8 * 127 * 4
+    n = 2 * chunk + extra if frame_len == 64 else chunk + extra
+    g = torch.Generator(device=DEV)
+    g.manual_seed(frame_len)
+    d = torch.randint(0, 256, (n * frame_len,), dtype=torch.uint8, device=DEV, generator=g)
+    engine.seal_fixed(d, frame_len, n=n)
+    flips = torch.tensor(sorted({f for f in (0, 1, chunk - 1, chunk, chunk + 1, n - 4, n - 1) if 0 <= f < n}),
+                         device=DEV)
+    assert int(flips.max()) < n
+    d[flips * frame_len + 2] ^= 0x40
+    crc, valid = engine.crc_fixed(d, frame_len, n=n)
+    torch.cuda.synchronize()
+    v = valid.cpu().numpy()
+    expect = np.ones(n, np.uint8)
+    expect[flips.cpu().numpy()] = 0
+    assert np.array_equal(v, expect)
+    host = d.cpu().numpy()
+    for lo in (0, chunk - 8, chunk - 2, n - 12):
+        ref_crc, ref_valid = oracle.validate_fixed(host[lo * frame_len:], frame_len, frame_len, n - lo if n - lo < 12 else 12)
+        got = crc[lo:lo + len(ref_crc)].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, ref_crc)

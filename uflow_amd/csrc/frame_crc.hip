@@ -448,15 +448,16 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   }
   const uint32_t tmask = (L.col == 15) ? 0u : 0xFFFFFFFFu;  // zero the trailer word in the CRC
 
-  // Results of the current run of 16 processed sets: lane (g, col=t) <- crc, and set index | valid
-  // << 31, of the run's t-th set, frame g.  Completed runs shift into hist_* registers and leave
-  // after the loop: a store inside the loop would make every later load wait vmcnt(0) (loads and
-  // stores share vmcnt and may complete out of order).
-  uint32_t acc_crc = 0, acc_qv = 0;
-  uint32_t hist_crc[kLeanRuns], hist_qv[kLeanRuns];
+  // Results: the k-th set this wave finishes goes to run r = k / 16, lane (g, col = k % 16) of
+  // res_crc[r] (crc) and res_qv[r] (set index | valid << 31), by selects on the wave-uniform r
+  // (no branch, no register shuffling in the loop).  They leave after the loop: a store inside
+  // the loop would make every later load wait vmcnt(0) (loads and stores share vmcnt and may
+  // complete out of order).
+  uint32_t res_crc[kLeanRuns], res_qv[kLeanRuns];
 #pragma unroll
-  for (int r = 0; r < kLeanRuns; r++) hist_crc[r] = hist_qv[r] = 0;
-  uint32_t t = 0, nhist = 0;  // sets in the current run, completed runs held (uniform)
+  for (int r = 0; r < kLeanRuns; r++) res_crc[r] = res_qv[r] = 0;
+  uint32_t k = 0;         // sets finished since the last flush (uniform)
+  uint32_t acc_crc = 0;   // (loads-only ablation 5)
   auto write_trailer = [&](uint64_t f, uint32_t crc) {  // seal: BE32 CRC into the frame's trailer
     uint8_t* a = p.wbytes + f * stride + n;
     if (((uintptr_t)a & 3u) == 0) {
@@ -479,41 +480,37 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       if (SEAL) write_trailer(f, crcs);
     }
   };
-  auto store_hist = [&]() {
+  auto store_all = [&]() {  // the k finished sets
 #pragma unroll
-    for (int r = 0; r < kLeanRuns; r++)
-      if ((uint32_t)r < nhist) store_run(kSetsPerRun, hist_crc[r], hist_qv[r]);
+    for (int r = 0; r < kLeanRuns; r++) {
+      const uint32_t first = 16u * (uint32_t)r;
+      if (first < k) store_run((int)min(k - first, 16u), res_crc[r], res_qv[r]);
+    }
   };
-  // Finish set q (this run's t-th): the trailer word (lane 15 of the frame's row) is broadcast to
-  // the row (DPP row_newbcast:15), so every lane of the frame has its validity.
-  // may_overflow: more than 16 * kLeanRuns sets may reach this wave's history (claimed schedule,
-  // the tail set); the static schedules never overflow inside the loop (host chunking), so
-  // their loop carries no store path.
+  // Finish set q: the trailer word (lane 15 of the frame's row) is broadcast to the row (DPP
+  // row_newbcast:15), so every lane of the frame has its validity.  may_overflow: more than
+  // 16 * kLeanRuns sets may reach this wave (claimed schedule, the tail set): a full result
+  // array is stored first, then vmcnt(0) so that no store stays pending into the loop; the
+  // static schedules never overflow inside the loop (host chunking), so their loop has no store.
   auto finish = [&](uint32_t q, const Chains& c, bool may_overflow) {
     const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
     const uint32_t ok = (len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
-    acc_crc = (L.col == (int)t) ? crc : acc_crc;
-    acc_qv = (L.col == (int)t) ? (q | (ok << 31)) : acc_qv;
-    if (++t == kSetsPerRun) {
-      // shift the run into the history (hist[0] newest); a full history is stored first, followed
-      // by an explicit vmcnt(0) so that no store stays pending into the loop (rare: > 128 sets
-      // per wave in one launch).
-      if (may_overflow && nhist == kLeanRuns) {
-        store_hist();
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-        nhist = 0;
-      }
-#pragma unroll
-      for (int r = kLeanRuns - 1; r > 0; r--) {
-        hist_crc[r] = hist_crc[r - 1];
-        hist_qv[r] = hist_qv[r - 1];
-      }
-      hist_crc[0] = acc_crc;
-      hist_qv[0] = acc_qv;
-      nhist++;
-      t = 0;
+    if (may_overflow && k == 16u * kLeanRuns) {
+      store_all();
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+      k = 0;
     }
+    const uint32_t run = k >> 4;
+    const bool mine = L.col == (int)(k & 15u);
+    const uint32_t qv = q | (ok << 31);
+#pragma unroll
+    for (int r = 0; r < kLeanRuns; r++) {
+      const bool sel = mine && run == (uint32_t)r;
+      res_crc[r] = sel ? crc : res_crc[r];
+      res_qv[r] = sel ? qv : res_qv[r];
+    }
+    k++;
   };
   // Frame-set processing from a loaded item (J blocks).
   auto compute = [&](uint32_t q, const ItemBuf<J>& b, Chains& c) {
@@ -708,19 +705,70 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       step(C, B, cZ, cX);
     }
   }
-  if (tail && blockIdx.x == gridDim.x - 1 && wid == wpb - 1) {  // the partial last set
-    ItemBuf<J> T;
-    load_tail(T);
-    compute(nfull, T, c);
-    finish(nfull, c, true);
-  }
   if (NO_FINISH) {  // keep the folded loads alive (tuning ablation)
     if (p.crc_out) p.crc_out[blockIdx.x * blockDim.x + threadIdx.x] = acc_crc;
     return;
   }
-  // Results: the partial run, then the history.
-  if (t > 0) store_run((int)t, acc_crc, acc_qv);
-  store_hist();
+  // The partial last set (grid's last wave; before any LDS reuse below), results stored directly.
+  if (tail && blockIdx.x == gridDim.x - 1 && wid == wpb - 1) {
+    ItemBuf<J> T;
+    load_tail(T);
+    compute(nfull, T, c);
+    const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
+    const uint32_t ok = (len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
+    const uint64_t f = (uint64_t)nfull * 4 + (uint64_t)L.grp;
+    if (L.col == 0 && f < p.nframes) {
+      if (p.crc_out) *as_global<g_u32w>(p.crc_out + f) = crc;
+      if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + f) = (uint8_t)ok;
+      if (SEAL) write_trailer(f, crc);
+    }
+  }
+  if (DYN) {
+    store_all();
+  } else {
+    // Static schedules: the workgroup's waves hold the results of its whole contiguous set range
+    // [blo, bhi).  Once every wave is done with the tables, the LDS stages them in frame order and
+    // the workgroup writes them with coalesced stores (each wave's own sets are 8 apart: storing
+    // them directly scatters 16-byte pieces over many lines at the end of the kernel).
+    uint32_t blo = q_lo, bhi = q_end;
+    if (!ILV) {
+      const uint64_t NW = (uint64_t)gridDim.x * wpb;
+      blo = s_fast + (uint32_t)((uint64_t)nfast * (blockIdx.x * wpb) / NW);
+      bhi = s_fast + (uint32_t)((uint64_t)nfast * ((blockIdx.x + 1) * wpb) / NW);
+    }
+    const uint32_t nfr = 4 * (bhi - blo);  // frames of the range (all < nframes)
+    uint32_t* lcrc = (uint32_t*)lds;
+    uint8_t* lval = (uint8_t*)lds + 4 * nfr;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#pragma unroll
+    for (int r = 0; r < kLeanRuns; r++) {
+      const uint32_t first = 16u * (uint32_t)r;
+      if (first < k && (uint32_t)L.col < min(k - first, 16u)) {
+        const uint32_t q = res_qv[r] & 0x7FFFFFFFu;
+        const uint32_t pos = (q - blo) * 4 + (uint32_t)L.grp;
+        lcrc[pos] = res_crc[r];
+        lval[pos] = (uint8_t)(res_qv[r] >> 31);
+        if (SEAL) write_trailer((uint64_t)q * 4 + (uint64_t)L.grp, res_crc[r]);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    const uint64_t f0 = (uint64_t)blo * 4;
+    if (p.crc_out)
+      for (uint32_t i = threadIdx.x; i < nfr; i += WAVES * 64) *as_global<g_u32w>(p.crc_out + f0 + i) = lcrc[i];
+    if (!SEAL && p.valid_out) {
+      if ((((uintptr_t)(p.valid_out + f0)) & 3u) == 0) {
+        for (uint32_t i = threadIdx.x; i < nfr / 4; i += WAVES * 64)
+          *as_global<g_u32w>((uint32_t*)(p.valid_out + f0) + i) = ((const uint32_t*)lval)[i];
+      } else {
+        for (uint32_t i = threadIdx.x; i < nfr; i += WAVES * 64) *as_global<g_u8w>(p.valid_out + f0 + i) = lval[i];
+      }
+    }
+  }
 
   if (DYN) {  // the workgroup's last wave resets the claim counters for the next launch
     // Every claim of this wave has returned (so has been performed) before `done` is counted.
