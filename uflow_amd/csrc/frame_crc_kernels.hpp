@@ -49,6 +49,7 @@ constexpr int kLeanWavesDefault = 8;
 constexpr int kSchedRange = 0;
 constexpr int kSchedClaim = 1;
 constexpr int kSchedInterleave = 2;
+constexpr int kSchedBlocked = 3;  // static: runs of 16 consecutive sets, interleaved over the waves
 constexpr int kLeanSchedDefault = kSchedInterleave;
 const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves);
 // Lean variable-length kernel (CSR offsets, any frame lengths; frames of 4..1532 B on the fast
@@ -56,7 +57,8 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
 // than 2^32 frames (host-chunked).
 // pairs: frames given as (start, end) pairs instead of CSR offsets (KernelParams::offsets holds
 // 2n words, frame_len the buffer length).  abl != 0: ablation variants of tuning builds.
-const void* varlen_kernel_symbol(bool seal, bool pairs, int abl);
+// sched/waves: kSchedClaim/16 (default) or kSchedBlocked/8 (A/B).
+const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

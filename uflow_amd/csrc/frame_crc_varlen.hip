@@ -95,27 +95,35 @@ constexpr int kAuxNT = 2;               // cache policy bits of the load: nt (st
 // register data, no block loads (offsets and geometry kept).
 // PAIRS: frame i = bytes[pairs[2i] .. pairs[2i+1]) (p.offsets holds the 2n pairs, p.frame_len the
 // buffer's byte length): any gapped layout, e.g. datagrams received into fixed-size slots.
-template <bool SEAL, bool PAIRS, int ABL>
-__global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelParams p) {
+// SCHED: kSchedClaim (sets handed out by a per-workgroup counter) or kSchedBlocked (static: wave
+// w takes the 16-set runs w, w + WAVES, w + 2 WAVES, ... of its workgroup's range, so every run of
+// results is 64 consecutive frames and leaves with coalesced stores).  WAVES: 8 or 16.
+template <bool SEAL, bool PAIRS, int ABL, int SCHED, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const KernelParams p) {
+  constexpr bool DYN = SCHED == kSchedClaim;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-  const StageSet<1024> sr = stage_load<1024>(p);
+  const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
   Lane L;
   init_lane(L, lds, p.G);
   constexpr int JM = kVlBlocks;
   const uint64_t nfr = p.nframes;
   const uint32_t nsets = (uint32_t)((nfr + 3) >> 2);  // < 2^30 (host chunks launches)
-  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wpb = WAVES;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t q_lo = (uint32_t)((uint64_t)nsets * blockIdx.x / gridDim.x);
   const uint32_t q_end = (uint32_t)((uint64_t)nsets * (blockIdx.x + 1) / gridDim.x);
-  uint32_t* ctr = p.ctr + blockIdx.x * kCtrWordsPerBlock;
+  uint32_t* ctr = DYN ? p.ctr + blockIdx.x * kCtrWordsPerBlock : nullptr;
   auto claim_issue = [&]() -> uint32_t {
     uint32_t v = 0;
-    if (L.lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (DYN && L.lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return v;
   };
-  // Sets 0..3 of each wave are static (lo + 16i + wid); the rest are claimed.
+  // Claimed: sets 0..3 of each wave are static (lo + wpb*i + wid); the rest are claimed.
   auto claim_set = [&](uint32_t v) -> uint32_t { return q_lo + 4 * wpb + __builtin_amdgcn_readfirstlane(v); };
+  // Blocked: the set after q in this wave's sequence (runs of kSetsPerRun consecutive sets).
+  auto next_set = [&](uint32_t q) -> uint32_t {
+    return ((q - q_lo) % kSetsPerRun == kSetsPerRun - 1) ? q + 1 + (wpb - 1) * kSetsPerRun : q + 1;
+  };
   // offsets[4q + g + (col & 1)] (clamped), or pairs[2(4q + g) + (col & 1)]: even lanes get the
   // frame's start, odd lanes its end.
   auto load_off = [&](uint32_t q) -> uint64_t {
@@ -317,9 +325,20 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   };
 
   // ---- prologue: static sets 0..3, claims for sets 4 and 5, data of sets 0 and 1 ----
-  uint32_t S0 = q_lo + wid, S1 = q_lo + wpb + wid, S2 = q_lo + 2 * wpb + wid, S3 = q_lo + 3 * wpb + wid, S4 = 0;
+  uint32_t S0, S1, S2, S3, S4 = 0;
+  if (DYN) {
+    S0 = q_lo + wid;
+    S1 = q_lo + wpb + wid;
+    S2 = q_lo + 2 * wpb + wid;
+    S3 = q_lo + 3 * wpb + wid;
+  } else {
+    S0 = q_lo + wid * kSetsPerRun;
+    S1 = next_set(S0);
+    S2 = next_set(S1);
+    S3 = next_set(S2);
+  }
   uint32_t cX = 0, cY = 0, cZ = 0;
-  cY = claim_issue();  // read in step 0 -> set 4
+  cY = claim_issue();  // read in step 0 -> set 4 (claimed schedule)
   cZ = claim_issue();  // read in step 1 -> set 5
   ItemBuf<JM> A, B, C;          // data ring: set m in slot m % 3
   uint64_t O0, O1, O2;          // offsets ring: set m in slot m % 3
@@ -346,8 +365,12 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   auto step = [&](ItemBuf<JM>& cur, uint32_t& gc, SetMeta& mc, const uint8_t*& bc, uint32_t& vc, uint64_t& ro,
                   uint64_t& wo, ItemBuf<JM>& fill, uint32_t& gf, SetMeta& mf, const uint8_t*& bf, uint32_t& vf,
                   uint32_t& c_issue, uint32_t& c_read) {
-    S4 = claim_set(c_read);
-    c_issue = claim_issue();
+    if (DYN) {
+      S4 = claim_set(c_read);
+      c_issue = claim_issue();
+    } else {
+      S4 = next_set(S3);
+    }
     wo = load_off(S4);
     {
       const uint8_t* sb;
@@ -381,7 +404,7 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   }
   if (t > 0) store_run((int)t);
 
-  {  // the workgroup's last wave resets the claim counters for the next launch
+  if (DYN) {  // the workgroup's last wave resets the claim counters for the next launch
     // Every claim of this wave has returned (so has been performed) before `done` is counted.
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
     uint32_t done = 0;
@@ -393,24 +416,50 @@ __global__ __launch_bounds__(1024) void frame_crc_varlen_kernel(const KernelPara
   }
 }
 
-template __global__ void frame_crc_varlen_kernel<false, false, 0>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<true, false, 0>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, true, 0>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<true, true, 0>(const KernelParams);
-#ifdef UFC_TUNING
-template __global__ void frame_crc_varlen_kernel<false, false, 1>(const KernelParams);
-template __global__ void frame_crc_varlen_kernel<false, false, 2>(const KernelParams);
-#endif
+#define UFC_VL_INST(SC, WV)                                                                    \
+  template __global__ void frame_crc_varlen_kernel<false, false, 0, SC, WV>(const KernelParams); \
+  template __global__ void frame_crc_varlen_kernel<true, false, 0, SC, WV>(const KernelParams);  \
+  template __global__ void frame_crc_varlen_kernel<false, true, 0, SC, WV>(const KernelParams);  \
+  template __global__ void frame_crc_varlen_kernel<true, true, 0, SC, WV>(const KernelParams);
+UFC_VL_INST(kSchedBlocked, 8)
+UFC_VL_INST(kSchedClaim, 16)
 
-const void* varlen_kernel_symbol(bool seal, bool pairs, int abl) {
+const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves) {
 #ifdef UFC_TUNING
-  if (!seal && !pairs && abl == 1) return (const void*)frame_crc_varlen_kernel<false, false, 1>;
-  if (!seal && !pairs && abl == 2) return (const void*)frame_crc_varlen_kernel<false, false, 2>;
+  if (!seal && !pairs && (abl == 1 || abl == 2)) {
+    // A/B: ablations for the schedule/waves pairs (instantiated by taking their addresses)
+    const bool blk = sched == kSchedBlocked;
+    if (waves == 8)
+      return abl == 1 ? (blk ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedBlocked, 8>
+                             : (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 8>)
+                      : (blk ? (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedBlocked, 8>
+                             : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 8>);
+    return abl == 1 ? (blk ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedBlocked, 16>
+                           : (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 16>)
+                    : (blk ? (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedBlocked, 16>
+                           : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 16>);
+  }
+  if (!seal && !pairs && abl == 0) {
+    if (sched == kSchedClaim && waves == 8) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 8>;
+    if (sched == kSchedBlocked && waves == 16) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedBlocked, 16>;
+  }
 #endif
   if (abl != 0) return nullptr;
-  if (pairs)
-    return seal ? (const void*)frame_crc_varlen_kernel<true, true, 0> : (const void*)frame_crc_varlen_kernel<false, true, 0>;
-  return seal ? (const void*)frame_crc_varlen_kernel<true, false, 0> : (const void*)frame_crc_varlen_kernel<false, false, 0>;
+  if (sched == kSchedBlocked && waves == 8) {
+    if (pairs)
+      return seal ? (const void*)frame_crc_varlen_kernel<true, true, 0, kSchedBlocked, 8>
+                  : (const void*)frame_crc_varlen_kernel<false, true, 0, kSchedBlocked, 8>;
+    return seal ? (const void*)frame_crc_varlen_kernel<true, false, 0, kSchedBlocked, 8>
+                : (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedBlocked, 8>;
+  }
+  if (sched == kSchedClaim && waves == 16) {
+    if (pairs)
+      return seal ? (const void*)frame_crc_varlen_kernel<true, true, 0, kSchedClaim, 16>
+                  : (const void*)frame_crc_varlen_kernel<false, true, 0, kSchedClaim, 16>;
+    return seal ? (const void*)frame_crc_varlen_kernel<true, false, 0, kSchedClaim, 16>
+                : (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 16>;
+  }
+  return nullptr;
 }
 
 }  // namespace ufc_dev

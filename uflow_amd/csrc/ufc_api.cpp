@@ -204,25 +204,33 @@ bool lean_varlen() {
 }
 
 int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream, bool pairs = false) {
-  int abl = 0;
+  // Claimed sets, 16 waves: measured fastest for mixed lengths (compute-heavy per set; DESIGN.md
+  // section 5.2).  UFC_VL_CFG=blocked8: the static blocked schedule at 8 waves (A/B).
+  int abl = 0, sched = ufc_dev::kSchedClaim, waves = 16;
+  if (const char* cfg = std::getenv("UFC_VL_CFG")) {
+    if (std::strcmp(cfg, "blocked8") == 0) {
+      sched = ufc_dev::kSchedBlocked;
+      waves = 8;
+    }
+  }
 #ifdef UFC_TUNING
   if (const char* ab = std::getenv("UFC_VL_ABL")) abl = std::atoi(ab);
+  if (const char* sc = std::getenv("UFC_VL_SCHED")) sched = std::atoi(sc);
+  if (const char* wv = std::getenv("UFC_VL_WAVES")) waves = std::atoi(wv);
 #endif
-  const void* fn = ufc_dev::varlen_kernel_symbol(seal, pairs, pairs ? 0 : abl);
+  const void* fn = ufc_dev::varlen_kernel_symbol(seal, pairs, pairs ? 0 : abl, sched, waves);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain;
   kp.nib_img = ctx->d_nib;
   kp.G = ctx->G;
   // Offsets stay absolute (relative to kp.bytes) in every chunk; a chunk only shifts the offsets
   // and output pointers.  Chunks keep set indices below 2^30.
-  const uint64_t waves_per_block = ufc_dev::kBlockThreads / 64;
+  const uint64_t waves_per_block = (uint64_t)waves;
   const uint64_t chunk = (uint64_t)1 << 31;
   const uint64_t total = kp.nframes;
   for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
-    // Every launch needs a full set (see lean_fixed_blocks): never leave a final chunk of < 4 frames.
-    if (total - f0 - c.nframes > 0 && total - f0 - c.nframes < 4) c.nframes -= 4;
     c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
@@ -233,7 +241,7 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
     if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
     if (blocks < 1) blocks = 1;
     void* args[] = {&c};
-    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kBlockThreads), args, 0, stream);
+    hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
   }
   return UFC_OK;
