@@ -364,11 +364,11 @@ def test_seal_host_varlen(engine):
 
 @pytest.mark.parametrize("frame_len,extra", [(64, 3), (1500, 1), (1472, 2)])
 def test_fixed_multi_launch(engine, frame_len, extra):
-    """Batches the host splits into several lean launches (8 waves x 127 sets x 4 frames per CU
+    """Batches the host splits into several lean launches (8 waves x 511 sets x 4 frames per CU
     each), with a remainder that would leave a final launch of < 4 frames: GPU seal, then GPU
     validate -> every frame valid except planted flips; a sample bit-exact vs the oracle."""
     ncu = torch.cuda.get_device_properties(0).multi_processor_count
-    chunk = ncu * 8 * 127 * 4
+    chunk = ncu * 8 * (16 * 32 - 1) * 4  # frames per launch at the default 8 waves (lean_runs(8) = 32)
     n = 2 * chunk + extra if frame_len == 64 else chunk + extra
     g = torch.Generator(device=DEV)
     g.manual_seed(frame_len)
@@ -384,8 +384,9 @@ def test_fixed_multi_launch(engine, frame_len, extra):
     expect = np.ones(n, np.uint8)
     expect[flips.cpu().numpy()] = 0
     assert np.array_equal(v, expect)
-    host = d.cpu().numpy()
     for lo in (0, chunk - 8, chunk - 2, n - 12):
-        ref_crc, ref_valid = oracle.validate_fixed(host[lo * frame_len:], frame_len, frame_len, n - lo if n - lo < 12 else 12)
-        got = crc[lo:lo + len(ref_crc)].cpu().numpy().view(np.uint32)
+        m = min(12, n - lo)
+        host = d[lo * frame_len:(lo + m) * frame_len].cpu().numpy()
+        ref_crc, ref_valid = oracle.validate_fixed(host, frame_len, frame_len, m)
+        got = crc[lo:lo + m].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, ref_crc)

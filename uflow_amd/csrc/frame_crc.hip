@@ -448,16 +448,17 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   }
   const uint32_t tmask = (L.col == 15) ? 0u : 0xFFFFFFFFu;  // zero the trailer word in the CRC
 
-  // Results: the k-th set this wave finishes goes to run r = k / 16, lane (g, col = k % 16) of
-  // res_crc[r] (crc) and res_qv[r] (set index | valid << 31), by selects on the wave-uniform r
-  // (no branch, no register shuffling in the loop).  They leave after the loop: a store inside
-  // the loop would make every later load wait vmcnt(0) (loads and stores share vmcnt and may
-  // complete out of order).
-  uint32_t res_crc[kLeanRuns], res_qv[kLeanRuns];
+  // Results: the current run of 16 finished sets in acc_* (lane (g, col = t) <- crc, and set index
+  // | valid << 31, of the run's t-th set, frame g); every 16 sets the run rolls into the history
+  // hist_*[0] (uniform branch, 2*RUNS moves).  They leave after the loop: a store inside the loop
+  // would make every later load wait vmcnt(0) (loads and stores share vmcnt and may complete out
+  // of order).  RUNS: 32 at 8 waves (256 VGPRs per wave), 8 at 16 waves (128).
+  constexpr int RUNS = lean_runs(WAVES);
+  uint32_t acc_crc = 0, acc_qv = 0;
+  uint32_t hist_crc[RUNS], hist_qv[RUNS];
 #pragma unroll
-  for (int r = 0; r < kLeanRuns; r++) res_crc[r] = res_qv[r] = 0;
-  uint32_t k = 0;         // sets finished since the last flush (uniform)
-  uint32_t acc_crc = 0;   // (loads-only ablation 5)
+  for (int r = 0; r < RUNS; r++) hist_crc[r] = hist_qv[r] = 0;
+  uint32_t t = 0, nhist = 0;  // sets in the current run, completed runs held (uniform)
   auto write_trailer = [&](uint64_t f, uint32_t crc) {  // seal: BE32 CRC into the frame's trailer
     uint8_t* a = p.wbytes + f * stride + n;
     if (((uintptr_t)a & 3u) == 0) {
@@ -480,37 +481,40 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       if (SEAL) write_trailer(f, crcs);
     }
   };
-  auto store_all = [&]() {  // the k finished sets
+  auto store_all = [&]() {  // the partial run, then the history
+    if (t > 0) store_run((int)t, acc_crc, acc_qv);
 #pragma unroll
-    for (int r = 0; r < kLeanRuns; r++) {
-      const uint32_t first = 16u * (uint32_t)r;
-      if (first < k) store_run((int)min(k - first, 16u), res_crc[r], res_qv[r]);
-    }
+    for (int r = 0; r < RUNS; r++)
+      if ((uint32_t)r < nhist) store_run(kSetsPerRun, hist_crc[r], hist_qv[r]);
   };
   // Finish set q: the trailer word (lane 15 of the frame's row) is broadcast to the row (DPP
   // row_newbcast:15), so every lane of the frame has its validity.  may_overflow: more than
-  // 16 * kLeanRuns sets may reach this wave (claimed schedule, the tail set): a full result
-  // array is stored first, then vmcnt(0) so that no store stays pending into the loop; the
-  // static schedules never overflow inside the loop (host chunking), so their loop has no store.
+  // 16 * RUNS sets may reach this wave (claimed schedule): a full history is stored first, then
+  // vmcnt(0) so that no store stays pending into the loop; the static schedules never overflow
+  // inside the loop (host chunking), so their loop has no store.
   auto finish = [&](uint32_t q, const Chains& c, bool may_overflow) {
     const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
     const uint32_t ok = (len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
-    if (may_overflow && k == 16u * kLeanRuns) {
-      store_all();
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
-      k = 0;
-    }
-    const uint32_t run = k >> 4;
-    const bool mine = L.col == (int)(k & 15u);
-    const uint32_t qv = q | (ok << 31);
+    acc_crc = (L.col == (int)t) ? crc : acc_crc;
+    acc_qv = (L.col == (int)t) ? (q | (ok << 31)) : acc_qv;
+    if (++t == kSetsPerRun) {
+      if (may_overflow && nhist == RUNS) {
+        t = 0;  // (acc_* is about to roll in; store_all must not store it as a partial run)
+        store_all();
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+        nhist = 0;
+      }
 #pragma unroll
-    for (int r = 0; r < kLeanRuns; r++) {
-      const bool sel = mine && run == (uint32_t)r;
-      res_crc[r] = sel ? crc : res_crc[r];
-      res_qv[r] = sel ? qv : res_qv[r];
+      for (int r = RUNS - 1; r > 0; r--) {
+        hist_crc[r] = hist_crc[r - 1];
+        hist_qv[r] = hist_qv[r - 1];
+      }
+      hist_crc[0] = acc_crc;
+      hist_qv[0] = acc_qv;
+      nhist++;
+      t = 0;
     }
-    k++;
   };
   // Frame-set processing from a loaded item (J blocks).
   auto compute = [&](uint32_t q, const ItemBuf<J>& b, Chains& c) {
@@ -743,17 +747,19 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#pragma unroll
-    for (int r = 0; r < kLeanRuns; r++) {
-      const uint32_t first = 16u * (uint32_t)r;
-      if (first < k && (uint32_t)L.col < min(k - first, 16u)) {
-        const uint32_t q = res_qv[r] & 0x7FFFFFFFu;
+    auto stage = [&](int cnt, uint32_t crcs, uint32_t qv) {
+      if (L.col < cnt) {
+        const uint32_t q = qv & 0x7FFFFFFFu;
         const uint32_t pos = (q - blo) * 4 + (uint32_t)L.grp;
-        lcrc[pos] = res_crc[r];
-        lval[pos] = (uint8_t)(res_qv[r] >> 31);
-        if (SEAL) write_trailer((uint64_t)q * 4 + (uint64_t)L.grp, res_crc[r]);
+        lcrc[pos] = crcs;
+        lval[pos] = (uint8_t)(qv >> 31);
+        if (SEAL) write_trailer((uint64_t)q * 4 + (uint64_t)L.grp, crcs);
       }
-    }
+    };
+    if (t > 0) stage((int)t, acc_crc, acc_qv);
+#pragma unroll
+    for (int r = 0; r < RUNS; r++)
+      if ((uint32_t)r < nhist) stage(kSetsPerRun, hist_crc[r], hist_qv[r]);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");

@@ -42,6 +42,8 @@ constexpr int kLeanDepthDefault = 2;
 // Results stay in registers until a wave's range is done: at most 16 * kLeanRuns sets per wave,
 // i.e. a launch covers at most (waves in the grid) * 16 * kLeanRuns * 4 frames (host-chunked).
 constexpr int kLeanRuns = 8;
+// Runs of history per wave by wave count: 32 at 8 waves, kLeanRuns at 16 (register budget).
+constexpr int lean_runs(int waves) { return waves == 8 ? 32 : kLeanRuns; }
 // waves: 16 (1024-thread workgroups) or 8 (512); one workgroup per CU either way (160 KiB LDS).
 constexpr int kLeanWavesDefault = 8;
 // Schedules of a workgroup's contiguous set range over its waves: per-wave contiguous ranges,

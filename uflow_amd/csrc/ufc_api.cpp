@@ -149,7 +149,7 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
   // keeps its absolute address, and chunks after the first may read the pad bytes before them.
   const uint64_t waves_per_block = (uint64_t)waves;
   // (16 * kLeanRuns - 1 sets per wave: the static schedules' histories never overflow in the loop)
-  const uint64_t chunk = (uint64_t)ctx->ncu * waves_per_block * (16 * ufc_dev::kLeanRuns - 1) * 4;
+  const uint64_t chunk = (uint64_t)ctx->ncu * waves_per_block * (16 * ufc_dev::lean_runs(waves) - 1) * 4;
   const uint64_t total = kp.nframes;
   for (uint64_t f0 = 0, step = 0; f0 < total; f0 += step) {
     ufc_dev::KernelParams c = kp;
