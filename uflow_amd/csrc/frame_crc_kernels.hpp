@@ -29,6 +29,7 @@ struct KernelParams {
   uint32_t* ctr;              // lean fixed kernel: per-workgroup claim counters (zero at launch)
   uint32_t front_ok;          // lean fixed kernel: the pad bytes before frame 0 are readable
   unsigned long long* dbg;    // tuning builds only: per-wave timestamps (nullptr in product use)
+  const uint64_t* offsets_csr;  // varlen sorted mode: the caller's CSR offsets (n+1), or nullptr for pairs
 };
 
 // Kernel entry for (JC 256-byte blocks per pipelined part, mode); nullptr if not instantiated.
@@ -59,8 +60,15 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
 // than 2^32 frames (host-chunked).
 // pairs: frames given as (start, end) pairs instead of CSR offsets (KernelParams::offsets holds
 // 2n words, frame_len the buffer length).  abl != 0: ablation variants of tuning builds.
-// sched/waves: kSchedClaim/16 (default) or kSchedBlocked/8 (A/B).
-const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves);
+// sched/waves: kSchedClaim/16 (default) or kSchedBlocked/8 (A/B).  sorted: the frames come as
+// run-sorted records (sort_runs below), p.offsets = the records.
+const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves, bool sorted);
+// Pre-pass of the sorted varlen mode: every run of 64 consecutive frames is ordered by its
+// frames' 256-byte block counts, so the main kernel's 4-frame sets share one block count (a set
+// otherwise computes its longest frame's blocks for all four).  Record r of run R (16 B):
+// {start (u64), len (u32), index in the run (bits 0..5) | past-the-end (bit 31)}.
+constexpr int kRunFrames = 64;
+int sort_runs(const uint64_t* offsets, bool pairs, uint64_t nframes, void* records, void* stream);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

@@ -38,6 +38,8 @@
 //   * Sets the fast path cannot take -- a frame shorter than 4 B or longer than 6 blocks, pad
 //     bytes before the buffer, the partial last set -- run byte-wise in the loop (rare: the loads
 //     and waits of that branch only drain this wave's pipeline).
+#include <type_traits>
+
 #include "frame_crc_dev.hpp"
 
 namespace ufc_dev {
@@ -98,16 +100,21 @@ constexpr int kAuxNT = 2;               // cache policy bits of the load: nt (st
 // SCHED: kSchedClaim (sets handed out by a per-workgroup counter) or kSchedBlocked (static: wave
 // w takes the 16-set runs w, w + WAVES, w + 2 WAVES, ... of its workgroup's range, so every run of
 // results is 64 consecutive frames and leaves with coalesced stores).  WAVES: 8 or 16.
-template <bool SEAL, bool PAIRS, int ABL, int SCHED, int WAVES>
+// SORTED: p.offsets holds run-sorted records (sort_runs_kernel): set q takes records 4q..4q+3,
+// whose frames share a block count; results go to frame 64 (q / 16) + (record's index in run).
+template <bool SEAL, bool PAIRS, int ABL, int SCHED, int WAVES, bool SORTED>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const KernelParams p) {
   constexpr bool DYN = SCHED == kSchedClaim;
+  using OffT = typename std::conditional<SORTED, uint4, uint64_t>::type;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
   Lane L;
   init_lane(L, lds, p.G);
   constexpr int JM = kVlBlocks;
   const uint64_t nfr = p.nframes;
-  const uint32_t nsets = (uint32_t)((nfr + 3) >> 2);  // < 2^30 (host chunks launches)
+  // < 2^30 (host chunks launches); sorted: every run's 16 sets, the last run padded
+  const uint32_t nsets = SORTED ? (uint32_t)((nfr + kRunFrames - 1) / kRunFrames) * (kRunFrames / 4)
+                                : (uint32_t)((nfr + 3) >> 2);
   const uint32_t wpb = WAVES;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t q_lo = (uint32_t)((uint64_t)nsets * blockIdx.x / gridDim.x);
@@ -126,13 +133,17 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   };
   // offsets[4q + g + (col & 1)] (clamped), or pairs[2(4q + g) + (col & 1)]: even lanes get the
   // frame's start, odd lanes its end.
-  auto load_off = [&](uint32_t q) -> uint64_t {
-    if (PAIRS) {
+  auto load_off = [&](uint32_t q) -> OffT {
+    if constexpr (SORTED) {  // this group's record (the same 16 bytes in its 16 lanes)
+      const u32x4 r = *as_global<g_u32x4>((const uint32_t*)p.offsets + 4 * (4 * (uint64_t)min(q, nsets - 1) + L.grp));
+      return make_uint4(r.x, r.y, r.z, r.w);
+    } else if (PAIRS) {
       const uint64_t f = min(4 * (uint64_t)min(q, nsets - 1) + (uint64_t)L.grp, nfr - 1);
       return *as_global<g_u64>(p.offsets + 2 * f + (uint64_t)(L.col & 1));
+    } else {
+      const uint64_t i = 4 * (uint64_t)min(q, nsets - 1) + (uint64_t)L.grp + (uint64_t)(L.col & 1);
+      return *as_global<g_u64>(p.offsets + (i < nfr ? i : nfr));
     }
-    const uint64_t i = 4 * (uint64_t)min(q, nsets - 1) + (uint64_t)L.grp + (uint64_t)(L.col & 1);
-    return *as_global<g_u64>(p.offsets + (i < nfr ? i : nfr));
   };
   auto frame_bounds = [&](uint64_t f, uint64_t& a, uint64_t& b) {
     a = PAIRS ? p.offsets[2 * f] : p.offsets[f];
@@ -140,33 +151,55 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   };
   const uint32_t lane16 = 16u * (uint32_t)L.col;
   // end of the batch's bytes (CSR: the last offset; pairs: the buffer length)
-  const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets + nfr);
+  const uint64_t buf_end =
+      PAIRS ? p.frame_len : *as_global<g_u64>((SORTED ? p.offsets_csr : p.offsets) + nfr);
 
   // Geometry of set q from its offsets: lane offset of block 0 (voff0), packed per-lane geometry,
   // the set's scalar base and uniform meta.  A set that is not live (past the range, or slow)
   // loads nothing (voff0 out of range).
-  auto geometry = [&](uint32_t q, uint64_t mine, const uint8_t*& sbase, uint32_t& voff0, SetMeta& m) -> uint32_t {
-    const uint32_t lo = (uint32_t)mine, hi = (uint32_t)(mine >> 32);
-    const uint32_t plo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-    const uint32_t phi = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0xB1, 0xF, 0xF, false);
-    const uint64_t other = (uint64_t)plo | ((uint64_t)phi << 32);
-    const uint64_t a = lane_pick64(kOddLanes, other, mine), b = lane_pick64(kOddLanes, mine, other);
-    const uint64_t a0 = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, 0) |
-                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), 0) << 32);
+  // (sorted: also the record's index in its run, bits 16..21)
+  auto geometry = [&](uint32_t q, OffT mine, const uint8_t*& sbase, uint32_t& voff0, SetMeta& m) -> uint32_t {
+    uint64_t a, b, a0;
+    bool dead = false;
+    uint32_t orig = 0;
+    auto lane_u64 = [](uint64_t v, int l) -> uint64_t {
+      return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32);
+    };
+    if constexpr (SORTED) {
+      a = (uint64_t)mine.x | ((uint64_t)mine.y << 32);
+      b = a + mine.z;
+      dead = (mine.w >> 31) != 0;
+      orig = mine.w & 63u;
+      // the set's frames are anywhere in their run: base on the lowest start
+      a0 = min(min(lane_u64(a, 0), lane_u64(a, 16)), min(lane_u64(a, 32), lane_u64(a, 48)));
+    } else {
+      const uint32_t lo = (uint32_t)mine, hi = (uint32_t)(mine >> 32);
+      const uint32_t plo = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+      const uint32_t phi = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0xB1, 0xF, 0xF, false);
+      const uint64_t other = (uint64_t)plo | ((uint64_t)phi << 32);
+      a = lane_pick64(kOddLanes, other, mine);
+      b = lane_pick64(kOddLanes, mine, other);
+      a0 = lane_u64(a, 0);
+    }
     const uint64_t len = b - a, rel = a - a0;
     const uint32_t l32 = (uint32_t)min(len, (uint64_t)0x40000000u);
     const uint32_t n = l32 >= 4u ? l32 - 4u : l32;
     const uint32_t J = min((n + 8u + 255u) >> 8, 15u);
     const uint32_t pad = (J * 256u - (n + 4u)) & 511u;
     const uint32_t dl = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - pad)) & 3u;
-    const bool bad = l32 < 4u || J > (uint32_t)JM || a < (uint64_t)pad || rel > (1u << 20) || b + 3 > buf_end;
+    const bool bad = dead || l32 < 4u || J > (uint32_t)JM || a < (uint64_t)pad || rel > (1u << 20) || b + 3 > buf_end;
     m.slow = __builtin_amdgcn_ballot_w64(bad) != 0;
     m.Jset = max(max(__builtin_amdgcn_readlane((int)J, 0), __builtin_amdgcn_readlane((int)J, 16)),
                  max(__builtin_amdgcn_readlane((int)J, 32), __builtin_amdgcn_readlane((int)J, 48)));
     const bool live = q < q_end && !m.slow;
     sbase = p.bytes + a0 - kVlBias;
     voff0 = live ? (uint32_t)rel + kVlBias - pad + dl + lane16 : kVlOob;
-    return pad | (J << 9) | ((l32 >= 5u ? 1u : 0u) << 13) | (dl << 14);
+    return pad | (J << 9) | ((l32 >= 5u ? 1u : 0u) << 13) | (dl << 14) | (orig << 16);
+  };
+  // Frame index of this lane's group in set q (results are recorded by frame, not by set).
+  auto frame_of = [&](uint32_t q, uint32_t geo) -> uint32_t {
+    return SORTED ? (q / (kRunFrames / 4)) * kRunFrames + ((geo >> 16) & 63u) : q;
   };
   // The 6 block loads of a set: blocks past the frame's J (and every block of a set that is not
   // live) are out of range.
@@ -199,7 +232,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   uint32_t acc_crc = 0, acc_qv = 0;
   uint32_t t = 0;  // sets in the current run (uniform)
   auto store_run = [&](int cnt) {
-    const uint64_t f = (uint64_t)(acc_qv & 0x3FFFFFFFu) * 4 + (uint64_t)L.grp;
+    // (sorted: qv holds the frame index; else the set index)
+    const uint64_t f = SORTED ? (uint64_t)(acc_qv & 0x3FFFFFFFu) : (uint64_t)(acc_qv & 0x3FFFFFFFu) * 4 + (uint64_t)L.grp;
     if (L.col < cnt && f < nfr && !(acc_qv & 0x40000000u)) {
       if (p.crc_out) st_u32_hidden(p.crc_out + f, acc_crc);
       if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_qv >> 31);
@@ -283,10 +317,20 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   // Byte path for set q: loads restricted to each frame, any length; results stored at once,
   // followed by vmcnt(0) so that no visible store stays pending.
   auto slow_set = [&](uint32_t q) {
-    const uint64_t fr = 4 * (uint64_t)q + (uint64_t)L.grp;
-    const uint64_t f = fr < nfr ? fr : nfr - 1;
-    uint64_t a, b;
-    frame_bounds(f, a, b);
+    uint64_t fr, a, b;
+    bool store_ok;
+    if constexpr (SORTED) {  // the record again (its ring slot has been reused by now)
+      const u32x4 r = *as_global<g_u32x4>((const uint32_t*)p.offsets + 4 * (4 * (uint64_t)q + L.grp));
+      a = (uint64_t)r.x | ((uint64_t)r.y << 32);
+      b = a + r.z;
+      fr = (uint64_t)(q / (kRunFrames / 4)) * kRunFrames + (r.w & 63u);
+      store_ok = (r.w >> 31) == 0;
+    } else {
+      fr = 4 * (uint64_t)q + (uint64_t)L.grp;
+      const uint64_t f = fr < nfr ? fr : nfr - 1;
+      frame_bounds(f, a, b);
+      store_ok = fr < nfr;
+    }
     const FrameDesc d = make_desc(a, b >= a ? b - a : 0);
     const int nb = max(max(__builtin_amdgcn_readlane(d.J, 0), __builtin_amdgcn_readlane(d.J, 16)),
                        max(__builtin_amdgcn_readlane(d.J, 32), __builtin_amdgcn_readlane(d.J, 48)));
@@ -310,7 +354,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
     }
     const uint32_t crc = ~group_lin(L, ce);
     const uint32_t ok = (d.len >= 5u && __builtin_bswap32(ce.tr) == crc) ? 1u : 0u;
-    if (L.col == 15 && fr < nfr) {
+    if (L.col == 15 && store_ok) {
       if (p.crc_out) *as_global<g_u32w>(p.crc_out + fr) = crc;
       if (!SEAL && p.valid_out) *as_global<g_u8w>(p.valid_out + fr) = (uint8_t)ok;
       if (SEAL && d.len >= 4u) {
@@ -341,13 +385,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   cY = claim_issue();  // read in step 0 -> set 4 (claimed schedule)
   cZ = claim_issue();  // read in step 1 -> set 5
   ItemBuf<JM> A, B, C;          // data ring: set m in slot m % 3
-  uint64_t O0, O1, O2;          // offsets ring: set m in slot m % 3
+  OffT O0, O1, O2;              // offsets (sorted: record) ring: set m in slot m % 3
   uint32_t g0, g1, g2;          // per-lane geometry ring
   SetMeta m0, m1, m2;           // uniform meta ring
   uint32_t v0 = 0, v1 = 0, v2 = 0;                               // seal: voff0 ring
   const uint8_t *b0 = p.bytes, *b1 = p.bytes, *b2 = p.bytes;  // seal: scalar base ring
   {
-    const uint64_t o0 = load_off(S0), o1 = load_off(S1);
+    const OffT o0 = load_off(S0), o1 = load_off(S1);
     O2 = load_off(S2);
     O0 = load_off(S3);
     uint32_t vo;
@@ -362,8 +406,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   stage_store(sr, lds);
 
   // One step (see the header comment).  cur/gc/mc: set S0; ro/fill/gf/mf: set S2; wo: set S4.
-  auto step = [&](ItemBuf<JM>& cur, uint32_t& gc, SetMeta& mc, const uint8_t*& bc, uint32_t& vc, uint64_t& ro,
-                  uint64_t& wo, ItemBuf<JM>& fill, uint32_t& gf, SetMeta& mf, const uint8_t*& bf, uint32_t& vf,
+  auto step = [&](ItemBuf<JM>& cur, uint32_t& gc, SetMeta& mc, const uint8_t*& bc, uint32_t& vc, OffT& ro,
+                  OffT& wo, ItemBuf<JM>& fill, uint32_t& gf, SetMeta& mf, const uint8_t*& bf, uint32_t& vf,
                   uint32_t& c_issue, uint32_t& c_read) {
     if (DYN) {
       S4 = claim_set(c_read);
@@ -384,7 +428,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
       if (!mc.slow) {
         const uint2 r = compute(gc, mc.Jset, cur);
         if (SEAL) seal_trailer(bc, vc, gc, r.x);
-        record(r.x, S0 | (r.y << 31));
+        record(r.x, frame_of(S0, gc) | (r.y << 31));
       } else {
         slow_set(S0);
         record(0u, S0 | 0x40000000u);
@@ -416,50 +460,99 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   }
 }
 
-#define UFC_VL_INST(SC, WV)                                                                    \
-  template __global__ void frame_crc_varlen_kernel<false, false, 0, SC, WV>(const KernelParams); \
-  template __global__ void frame_crc_varlen_kernel<true, false, 0, SC, WV>(const KernelParams);  \
-  template __global__ void frame_crc_varlen_kernel<false, true, 0, SC, WV>(const KernelParams);  \
-  template __global__ void frame_crc_varlen_kernel<true, true, 0, SC, WV>(const KernelParams);
-UFC_VL_INST(kSchedBlocked, 8)
-UFC_VL_INST(kSchedClaim, 16)
+#define UFC_VL_INST(SC, WV, SO)                                                                    \
+  template __global__ void frame_crc_varlen_kernel<false, false, 0, SC, WV, SO>(const KernelParams); \
+  template __global__ void frame_crc_varlen_kernel<true, false, 0, SC, WV, SO>(const KernelParams);  \
+  template __global__ void frame_crc_varlen_kernel<false, true, 0, SC, WV, SO>(const KernelParams);  \
+  template __global__ void frame_crc_varlen_kernel<true, true, 0, SC, WV, SO>(const KernelParams);
+UFC_VL_INST(kSchedClaim, 16, true)
+UFC_VL_INST(kSchedClaim, 16, false)
+UFC_VL_INST(kSchedBlocked, 8, false)
 
-const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves) {
+const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves, bool sorted) {
 #ifdef UFC_TUNING
-  if (!seal && !pairs && (abl == 1 || abl == 2)) {
+  if (!seal && !pairs && (abl == 1 || abl == 2) && !sorted) {
     // A/B: ablations for the schedule/waves pairs (instantiated by taking their addresses)
     const bool blk = sched == kSchedBlocked;
     if (waves == 8)
-      return abl == 1 ? (blk ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedBlocked, 8>
-                             : (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 8>)
-                      : (blk ? (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedBlocked, 8>
-                             : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 8>);
-    return abl == 1 ? (blk ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedBlocked, 16>
-                           : (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 16>)
-                    : (blk ? (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedBlocked, 16>
-                           : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 16>);
+      return abl == 1 ? (blk ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedBlocked, 8, false>
+                             : (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 8, false>)
+                      : (blk ? (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedBlocked, 8, false>
+                             : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 8, false>);
+    return abl == 1 ? (blk ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedBlocked, 16, false>
+                           : (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 16, false>)
+                    : (blk ? (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedBlocked, 16, false>
+                           : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 16, false>);
   }
-  if (!seal && !pairs && abl == 0) {
-    if (sched == kSchedClaim && waves == 8) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 8>;
-    if (sched == kSchedBlocked && waves == 16) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedBlocked, 16>;
+  if (!seal && !pairs && (abl == 1 || abl == 2) && sorted && sched == kSchedClaim && waves == 16)
+    return abl == 1 ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 16, true>
+                    : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 16, true>;
+  if (!seal && !pairs && abl == 0 && !sorted) {
+    if (sched == kSchedClaim && waves == 8) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 8, false>;
+    if (sched == kSchedBlocked && waves == 16) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedBlocked, 16, false>;
   }
 #endif
   if (abl != 0) return nullptr;
-  if (sched == kSchedBlocked && waves == 8) {
-    if (pairs)
-      return seal ? (const void*)frame_crc_varlen_kernel<true, true, 0, kSchedBlocked, 8>
-                  : (const void*)frame_crc_varlen_kernel<false, true, 0, kSchedBlocked, 8>;
-    return seal ? (const void*)frame_crc_varlen_kernel<true, false, 0, kSchedBlocked, 8>
-                : (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedBlocked, 8>;
+#define UFC_VL_PICK(SC, WV, SO)                                                          \
+  if (sched == SC && waves == WV && sorted == SO) {                                      \
+    if (pairs)                                                                           \
+      return seal ? (const void*)frame_crc_varlen_kernel<true, true, 0, SC, WV, SO>      \
+                  : (const void*)frame_crc_varlen_kernel<false, true, 0, SC, WV, SO>;    \
+    return seal ? (const void*)frame_crc_varlen_kernel<true, false, 0, SC, WV, SO>       \
+                : (const void*)frame_crc_varlen_kernel<false, false, 0, SC, WV, SO>;     \
   }
-  if (sched == kSchedClaim && waves == 16) {
-    if (pairs)
-      return seal ? (const void*)frame_crc_varlen_kernel<true, true, 0, kSchedClaim, 16>
-                  : (const void*)frame_crc_varlen_kernel<false, true, 0, kSchedClaim, 16>;
-    return seal ? (const void*)frame_crc_varlen_kernel<true, false, 0, kSchedClaim, 16>
-                : (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 16>;
-  }
+  UFC_VL_PICK(kSchedClaim, 16, true)
+  UFC_VL_PICK(kSchedClaim, 16, false)
+  UFC_VL_PICK(kSchedBlocked, 8, false)
+#undef UFC_VL_PICK
   return nullptr;
+}
+
+// ---- sorted mode pre-pass: one wave per run of 64 frames ----
+// Key = the frame's block count J (1..6); 7 = a frame the fast path cannot take (shorter than
+// 4 B, longer than 6 blocks); 8 = past the end of the batch.  Stable counting sort by ballots.
+template <bool PAIRS>
+__global__ __launch_bounds__(256) void sort_runs_kernel(const uint64_t* offsets, uint64_t nframes, uint4* rec) {
+  const uint64_t run = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const uint64_t nruns = (nframes + kRunFrames - 1) / kRunFrames;
+  if (run >= nruns) return;  // (whole waves)
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t f = run * kRunFrames + lane;
+  const bool live = f < nframes;
+  uint64_t a = 0, b = 0;
+  if (live) {
+    a = PAIRS ? offsets[2 * f] : offsets[f];
+    b = PAIRS ? offsets[2 * f + 1] : offsets[f + 1];
+  }
+  const uint64_t len = b >= a ? b - a : 0;
+  const uint64_t n4 = len >= 4 ? len - 4 : len;
+  const uint64_t J = (n4 + 8 + 255) >> 8;
+  const uint32_t key = !live ? 8u : ((len >= 4 && len < 0x40000000ull && J <= (uint64_t)kVlBlocks) ? (uint32_t)J : 7u);
+  uint32_t below = 0, rank_in = 0;
+#pragma unroll
+  for (uint32_t k = 1; k <= 8; k++) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(key == k);
+    const uint32_t c = (uint32_t)__builtin_popcountll(m);
+    below += (k < key) ? c : 0u;
+    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    rank_in = (k == key) ? r : rank_in;
+  }
+  const uint32_t rank = below + rank_in;
+  rec[run * kRunFrames + rank] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)min(len, (uint64_t)0xFFFFFFFFu),
+                                            lane | (live ? 0u : 0x80000000u));
+}
+
+int sort_runs(const uint64_t* offsets, bool pairs, uint64_t nframes, void* records, void* stream) {
+  const uint64_t nruns = (nframes + kRunFrames - 1) / kRunFrames;
+  if (nruns == 0) return 0;
+  const unsigned blocks = (unsigned)((nruns + 3) / 4);
+  if (pairs)
+    hipLaunchKernelGGL(sort_runs_kernel<true>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, offsets, nframes,
+                       (uint4*)records);
+  else
+    hipLaunchKernelGGL(sort_runs_kernel<false>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, offsets, nframes,
+                       (uint4*)records);
+  return (int)hipGetLastError();
 }
 
 }  // namespace ufc_dev
