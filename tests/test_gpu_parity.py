@@ -390,3 +390,18 @@ def test_fixed_multi_launch(engine, frame_len, extra):
         ref_crc, ref_valid = oracle.validate_fixed(host, frame_len, frame_len, m)
         got = crc[lo:lo + m].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, ref_crc)
+
+
+@pytest.mark.parametrize("cfg", [{"UFC_VL_SORT": "1"}, {"UFC_VL_CFG": "blocked8"}])
+def test_varlen_alternate_modes(engine, monkeypatch, cfg):
+    """The varlen kernel's A/B modes (read at launch time): run-sorted records, and the static
+    blocked schedule at 8 waves -- mixed lengths, edge lengths, seal, gapped pairs."""
+    for k, v in cfg.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(91)
+    _varlen_case(engine, rng, rng.integers(64, 1501, size=20_003).tolist(), flip_every=97)
+    lens = [0, 1, 2, 3, 4, 5, 6, 255, 256, 257, 258, 259, 260, 1472, 8192, 0, 9, 3000, 1, 1532, 1533] * 9
+    rng.shuffle(lens)
+    _varlen_case(engine, rng, lens, seal=False)
+    test_seal_varlen(engine)
+    test_pairs_gapped_layout(engine)
