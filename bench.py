@@ -109,28 +109,38 @@ def main():
         dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm
 
     from uflow_amd.batch import FrameCrcEngine
-    from uflow_amd.shard import gather_to_root
+    from uflow_amd.shard import ShardGatherer
 
     eng = FrameCrcEngine(local)
     n, L = a.frames_per_gpu, a.frame_len
     total = n * world
     frames = make_frames(eng, n, L, rank, a.flip_every, dev)
+    # N > 1: the kernel writes into a ShardGatherer slot and the slot's RCCL gather to rank 0 runs
+    # asynchronously, overlapping the next step's kernel (two slots, nothing allocated per step).
+    gat = ShardGatherer(n, dev) if world > 1 else None
     crc = torch.empty(n, dtype=torch.int32, device=dev)
     valid = torch.empty(n, dtype=torch.uint8, device=dev)
+    k_step = [0]
 
     def step(ev=None):
+        i = k_step[0] % 2
+        k_step[0] += 1
+        c_out, v_out = crc, valid
+        if gat is not None:
+            gat.wait(i)  # the slot's previous gather has finished reading it
+            c_out, v_out = gat.outputs(i)
         if ev is not None:
             ev[0].record()
-        eng.crc_fixed(frames, L, n=n, crc_out=crc, valid_out=valid)
+        eng.crc_fixed(frames, L, n=n, crc_out=c_out, valid_out=v_out)
         if ev is not None:
             ev[1].record()
-        if world > 1:
-            gather_to_root(crc, total)
-            gather_to_root(valid, total)
+        if gat is not None:
+            gat.start(i)
+        return i
 
     t_settle = time.perf_counter()
     while (time.perf_counter() - t_settle) * 1e3 < a.settle_ms:
-        eng.crc_fixed(frames, L, n=n, crc_out=crc, valid_out=valid)
+        step()
         torch.cuda.synchronize(dev)
     for _ in range(a.warmup):
         step()
@@ -139,8 +149,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
+    last = 0
     for i in range(a.steps):
-        step(evs[i])
+        last = step(evs[i])
+    if gat is not None:
+        gat.wait_all()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -153,10 +166,16 @@ def main():
     kern_all = np.array([e0.elapsed_time(e1) for e0, e1 in evs])
     kern_ms = float(np.mean(kern_all))
 
-    # correctness of this rank's shard: every flip_every-th frame invalid, all others valid
+    # correctness of this rank's shard: every flip_every-th frame invalid, all others valid; on
+    # rank 0 for N > 1 also the gathered flags of every rank
+    if gat is not None:
+        crc, valid = gat.outputs(last)
     nvalid = int(valid.sum().item())
     expect = n - ((n + a.flip_every - 1) // a.flip_every if a.flip_every else 0)
     ok = nvalid == expect
+    if gat is not None and rank == 0:
+        g_crc, g_valid = gat.gathered(last)
+        ok = ok and int(g_valid.sum().item()) == world * expect and bool(torch.equal(g_crc[:n], crc))
 
     result = None
     if rank == 0:
@@ -178,10 +197,12 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": f"synthetic: torch Philox random bytes (seed 0x5EED0001+rank), BE CRC trailers sealed on "
-                    f"device, 1 bit flipped in every {a.flip_every}th frame; valid flags checked: {ok}",
+                    f"device, 1 bit flipped in every {a.flip_every}th frame; valid flags checked"
+                    f"{' (and the gathered flags of every rank)' if world > 1 else ''}: {ok}",
             "config": {
                 "workload": f"config 2 (BASELINE.json configs[1]) per GPU: {n} x {L}-B frames, fixed stride, "
-                            f"device-resident; N>1: frame-sharded (weak), RCCL gather of CRC words + valid to rank 0",
+                            f"device-resident; N>1: frame-sharded (weak), RCCL gather of CRC words + valid to rank 0 "
+                            f"each step (async, overlapping the next step's kernel)",
                 "frames_per_gpu": n, "frame_len": L, "global_frames": total,
                 "parallelism": f"frame-sharded x{world}",
             },

@@ -84,3 +84,54 @@ def test_shard_range_partition():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard_range(10, 2, 2)
+
+
+def _pipelined_worker(rank, world, port, n, L, steps, q):
+    """bench.py's N>1 step loop with ShardGatherer: results written into the slot's views, async
+    gathers overlapping the next step, slots reused after wait()."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle
+        from uflow_amd.shard import ShardGatherer
+        buf = _batch(n * world, L)
+        g = ShardGatherer(n, torch.device("cpu"))
+        last = None
+        for k in range(steps):
+            i = k % 2
+            g.wait(i)
+            crc_v, val_v = g.outputs(i)
+            lo = rank * n
+            crc, valid = oracle.validate_fixed(buf[lo * L:(lo + n) * L], L, L, n)
+            crc_v.copy_(torch.from_numpy(crc.view(np.int32).copy()))
+            val_v.copy_(torch.from_numpy(valid.copy()))
+            g.start(i)
+            last = i
+        g.wait_all()
+        out = g.gathered(last)
+        if rank == 0:
+            q.put((out[0].numpy().view(np.uint32).copy(), out[1].numpy().copy()))
+        else:
+            assert out is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_gatherer_equals_single(world):
+    n, L, steps = 333, 120, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipelined_worker, args=(r, world, port, n, L, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got_crc, got_valid = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import oracle
+    ref_crc, ref_valid = oracle.validate_fixed(_batch(n * world, L), L, L, n * world)
+    assert np.array_equal(got_crc, ref_crc)
+    assert np.array_equal(got_valid, ref_valid)
