@@ -119,3 +119,22 @@ def test_ctx_create_without_gpu_fails_loudly():
     from uflow_amd.batch import FrameCrcEngine
     with pytest.raises(_native.NativeError):
         FrameCrcEngine(0)
+
+
+def test_c_caller_links_and_runs(tmp_path):
+    """The headers compile as strict C99 and a plain C program linked against libuflowcrc.so gets
+    the reference's KAT, gate, seal and builder behaviour (tests/c/c_abi_smoke.c) -- the shape of
+    the binding a Rust `extern "C"` block would use.  Host entry points only."""
+    import shutil
+    import subprocess
+    gcc = shutil.which("gcc")
+    if gcc is None:
+        pytest.skip("no gcc")
+    exe = tmp_path / "c_abi_smoke"
+    libdir = os.path.dirname(_native.LIB_PATH)
+    subprocess.run([gcc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", os.path.join(REPO, "include"),
+                    "-o", str(exe), os.path.join(REPO, "tests", "c", "c_abi_smoke.c"), "-L", libdir, "-luflowcrc",
+                    f"-Wl,-rpath,{libdir}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert "c abi ok" in r.stdout

@@ -359,7 +359,8 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 
 template <int J, bool SEAL, int DEPTH, int ABL_, int SCHED, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const KernelParams p) {
-  static_assert(DEPTH == 2 || DEPTH == 3, "pipeline depth (4 spills at J = 6)");
+  static_assert(DEPTH >= 1 && DEPTH <= 3, "pipeline depth (4 spills at J = 6)");
+  static_assert(DEPTH != 1 || SCHED != kSchedClaim, "depth 1: static schedules only");
   // Tuning ablation 5: loads only without the per-set finish.
   constexpr bool NO_FINISH = ABL_ == 5;
   constexpr int ABL = NO_FINISH ? kLeanAblLoads : ABL_;
@@ -688,7 +689,14 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   // Whole rounds of DEPTH steps with one uniform trip test (no early exits inside a round: they
   // would merge into the loop latch and poison the wait counts at the loop header).  The claim
   // ring rotates with period 3: step j issues into ring[j % 3] and reads ring[(j + 1) % 3].
-  if (DEPTH == 2 && !DYN) {  // static schedules: no claim ring, rounds of two steps
+  if (DEPTH == 1) {  // no prefetch: each wave loads a set, waits, computes (tuning A/B)
+    while (q_cur < q_end) {
+      compute(q_cur, A, c);
+      finish(q_cur, c, false);
+      q_cur += kInc;
+      load(q_cur, A);
+    }
+  } else if (DEPTH == 2 && !DYN) {  // static schedules: no claim ring, rounds of two steps
     while (q_cur < q_end) {
       step(A, B, cX, cY);
       step(B, A, cY, cZ);
@@ -884,6 +892,13 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
         {{(const void*)fixed_probe_kernel<2, 16, false>, (const void*)fixed_probe_kernel<3, 16, false>},
          {(const void*)fixed_probe_kernel<2, 16, true>, (const void*)fixed_probe_kernel<3, 16, true>}}};
     return ptab[waves == 16][abl == 4][depth - 2];
+  }
+  if (J == 6 && !seal && depth == 1 && sched == kSchedInterleave && (abl == 0 || abl == 1)) {
+    if (waves == 8)
+      return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 8>
+                      : (const void*)frame_crc_fixed_kernel<6, false, 1, kLeanAblLoads, kSchedInterleave, 8>;
+    return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 16>
+                    : (const void*)frame_crc_fixed_kernel<6, false, 1, kLeanAblLoads, kSchedInterleave, 16>;
   }
   if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedInterleave && abl == 5)
     return (const void*)frame_crc_fixed_kernel<6, false, 2, 5, kSchedInterleave, 8>;

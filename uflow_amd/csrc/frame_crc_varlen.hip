@@ -91,7 +91,10 @@ constexpr uint32_t kVlBias = 512;  // lane offsets are relative to (start of fra
 constexpr uint32_t kVlRecords = 0x7FFFFFF0u;
 constexpr uint32_t kVlOob = 0x80000000u;
 constexpr int kRsrcWord3 = 0x00020000;  // gfx9-family raw buffer descriptor word 3
-constexpr int kAuxNT = 2;               // cache policy bits of the load: nt (streaming)
+#ifndef UFC_VL_AUX
+#define UFC_VL_AUX 2
+#endif
+constexpr int kAuxNT = UFC_VL_AUX;      // cache policy bits of the loads: 2 = nt (streaming)
 
 // ABL (tuning builds only; results meaningless): bit 0 = loads + XOR fold, no CRC; bit 1 = CRC of
 // register data, no block loads (offsets and geometry kept).
