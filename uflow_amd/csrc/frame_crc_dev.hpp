@@ -275,23 +275,24 @@ constexpr int kLeanAblLoads = 1;
 constexpr int kLeanAblCompute = 2;
 
 // The tables are staged as 1024 chunks (one chain-table word replicated 32x + 32 B of the nibble
-// image each); a workgroup of THREADS threads stages 1024 / THREADS chunks per thread.
+// image each); a workgroup of THREADS threads stages ceil(1024 / THREADS) chunks per thread (the
+// last round partially when THREADS does not divide 1024, e.g. 768).
 struct StageRegs {
   uint32_t cv;
   u32x4 n0, n1;
 };
 template <int THREADS = 1024>
 struct StageSet {
-  static_assert(1024 % THREADS == 0, "workgroup size must divide 1024");
-  StageRegs r[1024 / THREADS];
+  static constexpr int kRounds = (1024 + THREADS - 1) / THREADS;
+  StageRegs r[kRounds];
 };
 
 template <int THREADS = 1024>
 __device__ __forceinline__ StageSet<THREADS> stage_load(const KernelParams& p) {
   StageSet<THREADS> s;
 #pragma unroll
-  for (int i = 0; i < 1024 / THREADS; i++) {
-    const int t = threadIdx.x + i * THREADS;
+  for (int i = 0; i < StageSet<THREADS>::kRounds; i++) {
+    const int t = min((int)threadIdx.x + i * THREADS, 1023);  // (a partial round re-reads chunk 1023)
     s.r[i].cv = *as_global<g_u32>(p.chain_tab + t);
     s.r[i].n0 = *as_global<g_u32x4>(p.nib_img + 8 * t);
     s.r[i].n1 = *as_global<g_u32x4>(p.nib_img + 8 * t + 4);
@@ -304,8 +305,9 @@ __device__ __forceinline__ StageSet<THREADS> stage_load(const KernelParams& p) {
 template <int THREADS = 1024>
 __device__ __forceinline__ void stage_store(const StageSet<THREADS>& s, char* lds) {
 #pragma unroll
-  for (int i = 0; i < 1024 / THREADS; i++) {
-    const int t = threadIdx.x + i * THREADS;
+  for (int i = 0; i < StageSet<THREADS>::kRounds; i++) {
+    const int t = (int)threadIdx.x + i * THREADS;
+    if (1024 % THREADS != 0 && t >= 1024) break;
     const StageRegs& r = s.r[i];
     const uint32_t k = (uint32_t)t >> 8, e = (uint32_t)t & 255u;
     const uint32_t cbase = kChainBase + (k >> 1) * 65536u + e * 256u + (k & 1u) * 128u;

@@ -474,7 +474,7 @@ UFC_VL_INST(kSchedBlocked, 8, false)
 
 const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves, bool sorted) {
 #ifdef UFC_TUNING
-  if (!seal && !pairs && (abl == 1 || abl == 2) && !sorted) {
+  if (!seal && !pairs && (abl == 1 || abl == 2) && !sorted && waves != 12) {
     // A/B: ablations for the schedule/waves pairs (instantiated by taking their addresses)
     const bool blk = sched == kSchedBlocked;
     if (waves == 8)
@@ -490,7 +490,11 @@ const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int 
   if (!seal && !pairs && (abl == 1 || abl == 2) && sorted && sched == kSchedClaim && waves == 16)
     return abl == 1 ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 16, true>
                     : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 16, true>;
+  if (!seal && !pairs && (abl == 1 || abl == 2) && !sorted && sched == kSchedClaim && waves == 12)
+    return abl == 1 ? (const void*)frame_crc_varlen_kernel<false, false, 1, kSchedClaim, 12, false>
+                    : (const void*)frame_crc_varlen_kernel<false, false, 2, kSchedClaim, 12, false>;
   if (!seal && !pairs && abl == 0 && !sorted) {
+    if (sched == kSchedClaim && waves == 12) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 12, false>;
     if (sched == kSchedClaim && waves == 8) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 8, false>;
     if (sched == kSchedBlocked && waves == 16) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedBlocked, 16, false>;
   }
