@@ -5,6 +5,7 @@ each.  Not the driver's bench (bench.py is); run on the GPU box:  python tools/b
            GiB/s on the sum of frame lengths, kernel time from HIP events.
   shard    config 4, one GPU's shard: 12.5M x 1500-B frames (18.75 GB) device-resident (the
            batch spans several launches of the lean kernel).
+  seal     the encode side of config 2: 1M x 1500-B frames sealed in place on the device.
   host     config 5's GPU leg: 1M x 1472-B frames (uflow's MAX_FRAME_SIZE) that start and end in
            host memory -> ufc_validate_host_varlen (H2D + CRC + D2H) from pinned and from pageable
            buffers; GiB/s of frame bytes including the copies.
@@ -93,6 +94,25 @@ def shard(eng, dev, n=12_500_000, L=1500, reps=10):
     return out
 
 
+def seal(eng, dev, n=1_000_000, L=1500, reps=20):
+    """The encode side on config 2's batch: ufc_seal_batch_fixed writes every frame's BE32
+    trailer in place (reads 1500 B, writes 4 B per frame); checked by validating afterwards."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED0004)
+    frames = torch.randint(0, 256, (n * L,), generator=g, device=dev, dtype=torch.uint8)
+    fn = lambda: eng.seal_fixed(frames, L, n=n)  # noqa: E731
+    fn()
+    torch.cuda.synchronize()
+    crc, valid = eng.crc_fixed(frames, L, n=n)
+    ok = int(valid.sum()) == n
+    ms = timed(fn, reps, torch.cuda.current_stream())
+    algo = n * L + 4 * n
+    return {"config": "2 (encode side): seal 1M x 1500-B frames in place, device-resident", "frames": n,
+            "kernel_ms": round(ms, 4), "GiB_s": round(n * L / ms / 1e-3 / 2**30, 1),
+            "algo_GB_s": round(algo / ms / 1e-3 / 1e9, 1), "hbm_frac": round(algo / ms / 1e-3 / 8e12, 4),
+            "valid_after_seal": ok}
+
+
 def host(eng, n=1_000_000, L=1472, reps=5):
     rng = np.random.default_rng(5)
     res = []
@@ -124,7 +144,7 @@ def host(eng, n=1_000_000, L=1472, reps=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="varlen,shard,host")
+    ap.add_argument("--only", default="varlen,shard,seal,host")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     eng = FrameCrcEngine(0)
@@ -136,6 +156,10 @@ def main():
     if "shard" in a.only:
         out.append(shard(eng, dev))
         print(json.dumps(out[-1]), flush=True)
+    if "seal" in a.only:
+        out.append(seal(eng, dev))
+        print(json.dumps(out[-1]), flush=True)
+        torch.cuda.empty_cache()
     if "host" in a.only:
         for r in host(eng):
             out.append(r)

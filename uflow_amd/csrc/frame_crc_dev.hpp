@@ -274,6 +274,17 @@ __device__ __forceinline__ void load_set(const uint8_t* sbase, uint32_t voff, It
 constexpr int kLeanAblLoads = 1;
 constexpr int kLeanAblCompute = 2;
 
+// Stores written as inline asm: hipcc's wait-count model never sees them, so it keeps counting
+// loads only (a store it could see would make every later load wait vmcnt(0), since loads and
+// stores share vmcnt and may complete out of order).  A hidden store can only make a counted
+// wait stricter (loads return in order), never looser.
+__device__ __forceinline__ void st_u32_hidden(uint32_t* a, uint32_t v) {
+  asm volatile("global_store_dword %0, %1, off" : : "v"(a), "v"(v));
+}
+__device__ __forceinline__ void st_u8_hidden(uint8_t* a, uint32_t v) {
+  asm volatile("global_store_byte %0, %1, off" : : "v"(a), "v"(v));
+}
+
 // The tables are staged as 1024 chunks (one chain-table word replicated 32x + 32 B of the nibble
 // image each); a workgroup of THREADS threads stages ceil(1024 / THREADS) chunks per thread (the
 // last round partially when THREADS does not divide 1024, e.g. 768).

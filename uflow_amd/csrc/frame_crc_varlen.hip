@@ -44,12 +44,6 @@
 
 namespace ufc_dev {
 
-__device__ __forceinline__ void st_u32_hidden(uint32_t* a, uint32_t v) {
-  asm volatile("global_store_dword %0, %1, off" : : "v"(a), "v"(v));
-}
-__device__ __forceinline__ void st_u8_hidden(uint8_t* a, uint32_t v) {
-  asm volatile("global_store_byte %0, %1, off" : : "v"(a), "v"(v));
-}
 
 // Per-lane pick between two uniform values by a constant lane mask (v_cndmask_b32).  Written as
 // asm: hipcc turns a select chain over the lane's group into an indexed scratch-memory table.
