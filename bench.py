@@ -1,9 +1,16 @@
 """Benchmark: device-resident frame-CRC throughput (BASELINE.json metric) on 1..N MI355X.
 
-One step = one pass of the batched CRC gate (crc + valid per frame, ufc_crc_batch_fixed) over
-this rank's shard of synthetic 1500-byte frames already resident in HBM, plus -- for N > 1 --
-the RCCL gather of the CRC words and valid flags to rank 0.  Weak scaling: every rank holds
---frames-per-gpu frames (default 1M = config 2 of BASELINE.json at N=1).
+One step = one pass of the batched CRC gate (CRC word + valid flag per frame) over frames already
+resident in HBM:
+  N = 1   config 2 (BASELINE.json configs[1]): 1M x 1500-B frames, ufc_crc_batch_fixed.
+  N > 1   config 4 (configs[3]): 100M x 1500-B frames sharded over the N GPUs (100M / N each,
+          strong scaling), ufc_crc_sharded = the gate on every rank's shard + the RCCL gather of
+          every CRC word and valid flag into global frame order on rank 0.  --frames-per-gpu gives
+          weak scaling instead.
+Frames are splitmix64 of the global byte index (seed 0x5EED0001 / 0x5EED0003, uflow_amd/synth.py),
+trailers sealed on the GPU, one bit flipped in every 1000th frame.  Results are checked against
+the CPU oracle (N = 1: every frame; N > 1: the valid flags of every frame and a sample of every
+rank's CRC words on rank 0); a mismatch makes the run fail.
 
 Launch:  python bench.py [--gpus 1 --steps 50 --warmup 10]
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -23,6 +30,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "HBM3E peak BW")
+CONFIG4_FRAMES = 100_000_000
 
 
 def parse():
@@ -30,28 +38,45 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--frames-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--frames-per-gpu", type=int, default=None,
+                    help="weak scaling: frames per GPU (default: N = 1 -> 1M, config 2)")
+    ap.add_argument("--global-frames", type=int, default=None,
+                    help="strong scaling: frames of the whole batch (default: N > 1 -> 100M, config 4)")
     ap.add_argument("--frame-len", type=int, default=1500)
     ap.add_argument("--flip-every", type=int, default=1000)
     ap.add_argument("--settle-ms", type=float, default=50.0,
-                    help="untimed back-to-back launches before the warmup steps: the clocks of a GPU "
-                         "coming out of idle step through a transient (kernels ~15%% slower for ~5 ms, "
-                         "DESIGN.md section 6); the timed steps measure the sustained rate")
+                    help="untimed back-to-back launches before the warmup steps: a GPU coming out of idle "
+                         "runs ~15%% slower for a few ms (DESIGN.md section 6); the timed steps measure the "
+                         "sustained rate")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU work of the baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of each CPU baseline leg")
     return ap.parse_args()
 
 
-def make_frames(engine, n, frame_len, rank, flip_every, dev):
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED0001 + rank)
-    frames = torch.randint(0, 256, (n * frame_len,), dtype=torch.uint8, device=dev, generator=g)
-    engine.seal_fixed(frames, frame_len, n=n)  # valid BE trailers
+def shard_of(total, rank, world):
+    return total * rank // world, total * (rank + 1) // world
+
+
+def make_frames(eng, first, n, L, seed, flip_every, dev):
+    """Frames [first, first + n) of the global batch, sealed on the GPU, global frames
+    0, flip_every, 2 flip_every, ... with one bit flipped (byte 17, mask 0x04)."""
+    from uflow_amd import synth
+    frames = synth.fixed_frames(n, L, seed, first_frame=first, device=dev)
+    eng.seal_fixed(frames, L, n=n)
     if flip_every:
-        idx = torch.arange(0, n, flip_every, device=dev, dtype=torch.int64) * frame_len + 17
-        frames[idx] ^= 0x04  # one flipped bit per flipped frame -> valid must be 0
+        g0 = (first + flip_every - 1) // flip_every * flip_every
+        local = torch.arange(g0 - first, n, flip_every, device=dev, dtype=torch.int64)
+        synth.flip_bits(frames, local * L)
     torch.cuda.synchronize(dev)
     return frames
+
+
+def expected_valid(first, n, flip_every):
+    v = np.ones(n, np.uint8)
+    if flip_every:
+        g0 = (first + flip_every - 1) // flip_every * flip_every
+        v[np.arange(g0 - first, n, flip_every)] = 0
+    return v
 
 
 def traffic_from_profile(frames, frame_len):
@@ -67,30 +92,44 @@ def traffic_from_profile(frames, frame_len):
     return None, None
 
 
-def cpu_baseline(frames_dev, n, frame_len, crc_dev, valid_dev, target_cpu_s):
-    """The oracle (C restatement of crc.rs:94-100, bytewise) on a bounded sample of the same
-    frames, frames split contiguously over T threads; checked against the GPU results."""
+def affinity_cpus():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_baseline(host, n, L, target_s):
+    """The oracle -- a C restatement of the reference's own loop, crc.rs:94-100 (one table load per
+    byte) behind the gate of serial/mod.rs:675-690 -- on the host cores: one thread, then every CPU
+    this process may run on, frames split contiguously; each leg on a bounded sample of config 2's
+    frames, repeated for about target_s seconds."""
     import oracle
-    sample = min(n, 200_000)
-    host = frames_dev[: sample * frame_len].cpu().numpy()
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
-    t0 = time.perf_counter()
-    crc, valid = oracle.validate_fixed_mt(host, frame_len, frame_len, sample, threads)
-    t1 = time.perf_counter()
-    reps = max(1, int(target_cpu_s / max(threads * (t1 - t0), 1e-3)))
-    t2 = time.perf_counter()
-    for _ in range(reps):
-        oracle.validate_fixed_mt(host, frame_len, frame_len, sample, threads)
-    t3 = time.perf_counter()
-    gcrc = crc_dev[:sample].cpu().numpy().view(np.uint32)
-    gval = valid_dev[:sample].cpu().numpy()
-    parity = bool(np.array_equal(gcrc, crc) and np.array_equal(gval, valid))
-    gib = sample * frame_len * reps / (t3 - t2) / 2**30
+
+    def leg(threads, sample):
+        buf = host[: sample * L]
+        t0 = time.perf_counter()
+        oracle.validate_fixed_mt(buf, L, L, sample, threads)
+        one = time.perf_counter() - t0
+        reps = max(1, int(target_s / max(one, 1e-4)))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            oracle.validate_fixed_mt(buf, L, L, sample, threads)
+        dt = time.perf_counter() - t0
+        return sample * L * reps / dt / 2**30, reps
+
+    threads = affinity_cpus()
+    s1 = min(n, 20_000)
+    v1, r1 = leg(1, s1)
+    sn = min(n, max(s1, 20_000 * threads))
+    vn, rn = leg(threads, sn)
     return {
-        "value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "sample": f"{sample} x {frame_len}-B frames (first frames of rank 0's shard) x {reps} reps, "
-                  f"bytewise table loop of crc.rs:94-100 in C (oracle/crc_oracle.c), frames split over "
-                  f"{threads} threads; results bit-equal to the GPU: {parity}",
+        "value": round(vn, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+        "single_core_value": round(v1, 4), "nproc": os.cpu_count(), "affinity_cpus": threads,
+        "sample": f"config 2 frames (first of the batch): {s1} x {L} B x {r1} reps on 1 thread, {sn} x {L} B x "
+                  f"{rn} reps on {threads} threads (all CPUs in this process's affinity; os.cpu_count() = "
+                  f"{os.cpu_count()}); bytewise table loop of crc.rs:94-100 in C (oracle/crc_oracle.c), "
+                  f"frames split contiguously over the threads",
     }
 
 
@@ -100,49 +139,73 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            print(f"--gpus {a.gpus} needs torch.distributed.run with {a.gpus} processes", file=sys.stderr)
-            sys.exit(2)
+        print(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run "
+              f"--nproc-per-node {a.gpus}", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm
+        dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm: barriers and the timing max
 
+    from uflow_amd import synth
     from uflow_amd.batch import FrameCrcEngine
-    from uflow_amd.shard import ShardGatherer
+    from uflow_amd.shard import ShardedGate, comm_id_create
 
     eng = FrameCrcEngine(local)
-    n, L = a.frames_per_gpu, a.frame_len
-    total = n * world
-    frames = make_frames(eng, n, L, rank, a.flip_every, dev)
-    # N > 1: the kernel writes into a ShardGatherer slot and the slot's RCCL gather to rank 0 runs
-    # asynchronously, overlapping the next step's kernel (two slots, nothing allocated per step).
-    gat = ShardGatherer(n, dev) if world > 1 else None
-    crc = torch.empty(n, dtype=torch.int32, device=dev)
-    valid = torch.empty(n, dtype=torch.uint8, device=dev)
+    L = a.frame_len
+    if a.frames_per_gpu is not None:
+        total, scaling = a.frames_per_gpu * world, "weak"
+    elif a.global_frames is not None:
+        total, scaling = a.global_frames, "strong"
+    elif world == 1:
+        total, scaling = 1_000_000, "weak"  # config 2
+    else:
+        total, scaling = CONFIG4_FRAMES, "strong"  # config 4
+    seed = synth.SEED_CONFIG2 if world == 1 else synth.SEED_CONFIG4
+    lo, hi = shard_of(total, rank, world)
+    n = hi - lo
+    frames = make_frames(eng, lo, n, L, seed, a.flip_every, dev)
+
+    gate = None
+    if world > 1:
+        idt = torch.zeros(128, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            idt.copy_(torch.frombuffer(bytearray(comm_id_create()), dtype=torch.uint8))
+        dist.broadcast(idt, src=0)
+        gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
+    # Outputs: two slots (step k writes slot k % 2 while the gather of step k - 1 may still read the
+    # other); rank 0's slots hold the whole batch in global order.
+    n_out = total if rank == 0 else n
+    slots = [(torch.empty(n_out, dtype=torch.int32, device=dev), torch.empty(n_out, dtype=torch.uint8, device=dev))
+             for _ in range(2 if world > 1 else 1)]
+    compute = torch.cuda.current_stream(dev)
+    gather = torch.cuda.Stream(dev) if world > 1 else None
+    gathered = [None, None]  # event on the gather stream after each slot's last gather
     k_step = [0]
 
     def step(ev=None):
-        i = k_step[0] % 2
+        i = k_step[0] % len(slots)
         k_step[0] += 1
-        c_out, v_out = crc, valid
-        if gat is not None:
-            gat.wait(i)  # the slot's previous gather has finished reading it
-            c_out, v_out = gat.outputs(i)
+        crc, valid = slots[i]
+        if gathered[i] is not None:
+            compute.wait_event(gathered[i])  # the slot's previous gather has finished with it
         if ev is not None:
-            ev[0].record()
-        eng.crc_fixed(frames, L, n=n, crc_out=c_out, valid_out=v_out)
+            ev[0].record(compute)
+        if gate is None:
+            eng.crc_fixed(frames, L, n=n, crc_out=crc, valid_out=valid)
+        else:
+            gate.crc_sharded(frames, L, total, crc, valid, root=0, stream=compute, gather_stream=gather)
+            e = torch.cuda.Event()
+            e.record(gather)
+            gathered[i] = e
         if ev is not None:
-            ev[1].record()
-        if gat is not None:
-            gat.start(i)
+            ev[1].record(compute)
         return i
 
-    # Settle: kernel only (no gather), so that ranks may run different numbers of iterations
-    # without mismatching their collectives.
+    # Settle: the gate alone (no collective), so ranks may run different numbers of iterations.
     t_settle = time.perf_counter()
     while (time.perf_counter() - t_settle) * 1e3 < a.settle_ms:
-        eng.crc_fixed(frames, L, n=n, crc_out=crc, valid_out=valid)
+        eng.crc_fixed(frames, L, n=n, crc_out=slots[0][0][:n], valid_out=slots[0][1][:n])
         torch.cuda.synchronize(dev)
     for _ in range(a.warmup):
         step()
@@ -154,8 +217,6 @@ def main():
     last = 0
     for i in range(a.steps):
         last = step(evs[i])
-    if gat is not None:
-        gat.wait_all()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -168,23 +229,48 @@ def main():
     kern_all = np.array([e0.elapsed_time(e1) for e0, e1 in evs])
     kern_ms = float(np.mean(kern_all))
 
-    # correctness of this rank's shard: every flip_every-th frame invalid, all others valid; on
-    # rank 0 for N > 1 also the gathered flags of every rank
-    if gat is not None:
-        crc, valid = gat.outputs(last)
-    nvalid = int(valid.sum().item())
-    expect = n - ((n + a.flip_every - 1) // a.flip_every if a.flip_every else 0)
-    ok = nvalid == expect
-    if gat is not None and rank == 0:
-        g_crc, g_valid = gat.gathered(last)
-        ok = ok and int(g_valid.sum().item()) == world * expect and bool(torch.equal(g_crc[:n], crc))
+    # ---- correctness (after the timed region) ----
+    import oracle
+    crc, valid = slots[last]
+    ok, parity = True, ""
+    if rank == 0:
+        h_valid = valid.cpu().numpy()
+        ok = bool(np.array_equal(h_valid, expected_valid(0, total, a.flip_every)))
+        h_crc = crc.cpu().numpy().view(np.uint32)
+        if world == 1:
+            host = frames.cpu().numpy()
+            ref_crc, ref_valid = oracle.validate_fixed_mt(host, L, L, n, min(64, affinity_cpus()))
+            exact = bool(np.array_equal(h_crc, ref_crc) and np.array_equal(h_valid, ref_valid))
+            parity = f"every frame bit-exact vs the CPU oracle: {exact}"
+        else:
+            # a sample of every rank's shard, regenerated here: the CRC word is compute(frame[..-4]),
+            # independent of the trailer, so the oracle needs only the (flipped) synthetic bytes
+            exact = True
+            for r in range(world):
+                rlo, rhi = shard_of(total, r, world)
+                for s0 in (rlo, (rlo + rhi) // 2, max(rlo, rhi - 2000)):
+                    m = min(2000, rhi - s0)
+                    sample = synth.fixed_frames(m, L, seed, first_frame=s0, device=dev)
+                    fl = np.nonzero(expected_valid(s0, m, a.flip_every) == 0)[0]
+                    if fl.size:
+                        synth.flip_bits(sample, torch.from_numpy(fl * L).to(dev))
+                    ref_crc, _ = oracle.validate_fixed(sample.cpu().numpy(), L, L, m)
+                    exact = exact and bool(np.array_equal(h_crc[s0:s0 + m], ref_crc))
+            parity = f"valid flags of all {total} frames + 3 x 2000 CRC words per rank bit-exact vs the oracle: {exact}"
+        ok = ok and exact
 
     result = None
     if rank == 0:
-        algo_bytes = n * L + n * 4 + n * 1  # frames read + crc words + valid bytes, per launch
+        algo_bytes = n * L + n * 4 + n * 1  # per launch group: frames read + crc words + valid bytes
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, tsrc = traffic_from_profile(n, L)
+        traffic, tsrc = traffic_from_profile(n, L) if world == 1 else (None, None)
         value = total * L / elapsed * a.steps / 2**30
+        cfg_name = (f"config 2 (BASELINE.json configs[1]): {n} x {L}-B frames, fixed stride, device-resident"
+                    if world == 1 and total == 1_000_000 else
+                    f"config 4 (BASELINE.json configs[3]): {total} x {L}-B frames sharded over {world} GPUs "
+                    f"({n} per GPU on rank 0), RCCL gather of every CRC word + valid flag to rank 0 in global "
+                    f"order (ufc_crc_sharded)" if total == CONFIG4_FRAMES else
+                    f"{total} x {L}-B frames over {world} GPU(s)")
         result = {
             "metric": "device-resident frame-CRC GiB/s (1500-B frames, validate: crc+valid per frame)",
             "value": round(value, 2),
@@ -195,40 +281,45 @@ def main():
             "settle_ms": a.settle_ms,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
-            "data": f"synthetic: torch Philox random bytes (seed 0x5EED0001+rank), BE CRC trailers sealed on "
-                    f"device, 1 bit flipped in every {a.flip_every}th frame; valid flags checked"
-                    f"{' (and the gathered flags of every rank)' if world > 1 else ''}: {ok}",
+            "data": f"synthetic: splitmix64 of the global byte index (seed {seed:#x}), BE CRC trailers sealed on "
+                    f"the GPU, 1 bit flipped in every {a.flip_every}th frame; {parity}; valid flags as planted: {ok}",
             "config": {
-                "workload": f"config 2 (BASELINE.json configs[1]) per GPU: {n} x {L}-B frames, fixed stride, "
-                            f"device-resident; N>1: frame-sharded (weak), RCCL gather of CRC words + valid to rank 0 "
-                            f"each step (async, overlapping the next step's kernel)",
+                "workload": cfg_name,
                 "frames_per_gpu": n, "frame_len": L, "global_frames": total,
                 "parallelism": f"frame-sharded x{world}",
             },
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8> (ufc_crc_batch_fixed)",
+                "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8> (ufc_crc_batch_fixed"
+                          + (", per chunk of ufc_crc_sharded" if world > 1 else "") + ")",
                 "kernel_avg_ms": round(kern_ms, 4),
                 "kernel_median_ms": round(float(np.median(kern_all)), 4),
                 "kernel_min_ms": round(float(np.min(kern_all)), 4),
                 "algorithmic_bytes_per_launch": algo_bytes,
+                "timed_on": "HIP events on the compute stream around each step's gate"
+                            + (" (all chunks of this rank's shard)" if world > 1 else ""),
                 **({"traffic_source": tsrc} if tsrc else {}),
             },
         }
         if world == 1 and not a.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(frames, n, L, crc, valid, a.cpu_seconds)
+            result["cpu_baseline"] = cpu_baseline(host, n, L, a.cpu_seconds)
+    if gate is not None:
+        gate.close()
     if world > 1:
+        okt = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
+        dist.broadcast(okt, src=0)
+        ok = int(okt.item()) == 0
         dist.barrier()
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
     eng.close()
     if not ok:
-        print(f"rank {rank}: valid count {nvalid} != expected {expect}", file=sys.stderr)
+        print(f"rank {rank}: results differ from the oracle / planted flips", file=sys.stderr)
         sys.exit(1)
 
 

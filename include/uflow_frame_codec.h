@@ -14,6 +14,9 @@
  *   ufc_parse_batch_host       <- the receive loops' Frame::read of every datagram (src/server/mod.rs:
  *                                 591-602, src/client/mod.rs:615-623), after the batched CRC gate
  *   ufc_parse_batch_varlen     <- the same parse on the GPU, device-resident frames
+ *   ufc_datagram_is_valid, UFC_ITEM_VALID
+ *                              <- src/half_connection/packet_receiver/mod.rs:12-30 `datagram_is_valid`,
+ *                                 applied by handle_datagram (:147-150) to every received datagram
  *
  * Conventions: as uflow_frame_crc.h.  A frame the reference would reject is data (ok = 0), never
  * an error; nothing is allocated per call except where stated (the device parse's scan scratch
@@ -78,10 +81,19 @@ typedef struct ufc_item {
   uint16_t channel_parent_lead;
   uint16_t fragment_id;
   uint16_t fragment_id_last;
-  uint16_t reserved;
+  uint16_t flags;               /* datagram: UFC_ITEM_VALID if datagram_is_valid (below); ack group: 0 */
   uint32_t data_offset;         /* datagram: payload offset in the frame; ack group: bitfield */
   uint32_t data_len;            /* datagram: payload bytes; ack group: 0 */
 } ufc_item;
+
+/* ufc_item.flags bit: the datagram passes the receive side's content check,
+ * src/half_connection/packet_receiver/mod.rs:12-30 `datagram_is_valid` (channel < 64; a nonzero
+ * channel_parent_lead needs window_parent_lead != 0 and channel_parent_lead >= window_parent_lead;
+ * fragment_id <= fragment_id_last; every fragment but the last exactly UFC_MAX_FRAGMENT_SIZE bytes;
+ * no payload over UFC_MAX_FRAGMENT_SIZE).  handle_datagram (:147-150) drops datagrams without it. */
+#define UFC_ITEM_VALID 1
+/* MAX_FRAGMENT_SIZE = MAX_FRAME_SIZE - DATA_FRAME_OVERHEAD - MAX_DATAGRAM_OVERHEAD (src/lib.rs:297). */
+#define UFC_MAX_FRAGMENT_SIZE 1448
 
 /* ---- scalar host entry points ---- */
 /* Frame::read: 1 = Some, 0 = None.  info is always written; up to items_cap items are written
@@ -92,6 +104,10 @@ int ufc_frame_read(const uint8_t* frame, size_t len, ufc_frame_info* info, ufc_i
  * gate's verdict for this frame.  Returns and fills as ufc_frame_read. */
 int ufc_frame_parse(const uint8_t* frame, size_t len, int crc_ok, ufc_frame_info* info, ufc_item* items,
                     size_t items_cap);
+
+/* datagram_is_valid (src/half_connection/packet_receiver/mod.rs:12-30) of a decoded datagram
+ * (form 0..2): 1 valid, 0 not (the parses store the same verdict in flags & UFC_ITEM_VALID). */
+int ufc_datagram_is_valid(const ufc_item* datagram);
 
 /* Fixed-size frames (every kind but data and ack) from info; writes the BE32 CRC trailer when
  * seal != 0, else 4 zero bytes (for a batched seal on the GPU).  Returns the frame length, 0 if

@@ -18,6 +18,8 @@
  *                             recvmmsg layout (fixed-size slots + lengths) of the receive loops
  *   ufc_seal_host_slots /     a flush's frames sealed in one batch before sendmmsg (the builders'
  *   ufc_seal_host_varlen      build(), build.rs:151-159, for every frame of half_connection/emit.rs)
+ *   ufc_crc_sharded           the gate over a batch sharded across the GPUs of a node (one process
+ *                             per GPU), CRC words + valid flags gathered to a root over RCCL
  *
  * Conventions (mirroring the reference):
  *   - All buffers are caller-owned; nothing is retained after a call returns (device calls:
@@ -32,9 +34,11 @@
  *     stream), allocate nothing per call, and never fall back to the CPU: without a usable
  *     MI355X (gfx950) device ufc_ctx_create fails with UFC_ERR_NO_DEVICE.
  *   - One ufc_ctx per device.  Device launches on different streams of one context are safe while
- *     fewer than 64 are in flight (each takes a claim-counter slot); ufc_validate_host_varlen
- *     uses the context's own streams and staging, one host thread at a time per context.  The
- *     scalar host functions are reentrant.
+ *     fewer than 64 are in flight (each takes a claim-counter slot); device scratch (batch parse,
+ *     sorted varlen mode) is kept per stream.  The host-buffer calls (ufc_validate_host_*,
+ *     ufc_seal_host_*) use the context's own streams and staging, one host thread at a time per
+ *     context; they are synchronous and, on error too, return only once no copy touches the
+ *     caller's buffers.  The scalar host functions are reentrant.
  */
 #ifndef UFLOW_FRAME_CRC_H
 #define UFLOW_FRAME_CRC_H
@@ -51,6 +55,7 @@ extern "C" {
 #define UFC_ERR_NO_DEVICE (-2)
 #define UFC_ERR_HIP (-3)
 #define UFC_ERR_NOMEM (-4)
+#define UFC_ERR_COMM (-5) /* RCCL missing or failed (multi-GPU entry points; see ufc_comm_last_error) */
 
 /* Frame constants from the reference (src/frame/serial/mod.rs:11-13, src/lib.rs:286-294). */
 #define UFC_FRAME_CRC_SIZE 4
@@ -73,6 +78,22 @@ int ufc_ctx_destroy(ufc_ctx* ctx);
 const char* ufc_error_string(int code);
 /* Last HIP error code seen by this context (0 if none). */
 int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
+
+/* Kernel-selection options of a context (A/B measurement and tests; the defaults are the measured
+ * fastest).  Results never depend on them.  Set between calls, not while work is queued. */
+#define UFC_OPT_FIXED_KERNEL 0   /* fixed-stride batches: */
+#define UFC_FIXED_AUTO 0         /*   lean kernel when eligible (default) */
+#define UFC_FIXED_GENERIC 1      /*   the generic kernel */
+#define UFC_FIXED_CLAIM16 2      /*   lean kernel, claimed schedule at 16 waves (round-1 default) */
+#define UFC_OPT_VARLEN_KERNEL 1  /* CSR / pairs batches: */
+#define UFC_VARLEN_AUTO 0        /*   default */
+#define UFC_VARLEN_GENERIC 1     /*   the generic kernel */
+#define UFC_VARLEN_SORTED 2      /*   frames sorted by block count within runs of 64 first */
+#define UFC_VARLEN_BLOCKED8 3    /*   static blocked schedule at 8 waves */
+#define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
+#define UFC_OPT_COUNT_ 3
+int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value);
+int ufc_ctx_get_option(const ufc_ctx* ctx, int option);
 
 /* ---- batched, device-resident ---- */
 /* Frame i occupies d_frames[i*stride .. i*stride + frame_len); stride >= frame_len.
@@ -109,6 +130,41 @@ int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_st
 int ufc_seal_host_slots(ufc_ctx* ctx, uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens, size_t n,
                         uint32_t* h_crc_scratch);
 int ufc_seal_host_varlen(ufc_ctx* ctx, uint8_t* h_bytes, const uint64_t* h_offsets, size_t n, uint32_t* h_crc_scratch);
+
+/* ---- multi-GPU: one process per GPU, frames sharded by index, RCCL gather to a root ----
+ * Replaces, for a batch spread over the GPUs of one node, the receive loop's per-datagram gate
+ * (src/server/mod.rs:591-602 -> Frame::read, serial/mod.rs:675-690).  Rank r owns the frames
+ * ufc_shard_range(n_total, nranks, r) = [n_total r / nranks, n_total (r+1) / nranks) of a batch of
+ * n_total fixed-length frames; the only exchange is the per-frame CRC word and valid flag of every
+ * frame, gathered into global frame order on the root over RCCL (xGMI point-to-point).  RCCL is
+ * loaded at run time (librccl.so.1); without it these calls return UFC_ERR_COMM. */
+#define UFC_COMM_ID_BYTES 128
+typedef struct ufc_comm ufc_comm;
+int ufc_shard_range(uint64_t n_total, int nranks, int rank, uint64_t* first, uint64_t* count);
+/* The gather pipeline's chunk `chunk` of rank `rank`'s shard: global frames [*first, *first + *count).
+ * Returns the number of chunks every shard of the batch is split into (1..16: one per <= 2^22 frames
+ * of a shard), or UFC_ERR_INVALID_ARG. */
+int ufc_shard_chunk(uint64_t n_total, int nranks, int rank, int chunk, uint64_t* first, uint64_t* count);
+/* On one rank: a fresh communicator id (ncclGetUniqueId), handed to every rank out of band. */
+int ufc_comm_id_create(uint8_t id[UFC_COMM_ID_BYTES]);
+/* Collective over the nranks processes (one per GPU, each with its own ufc_ctx). */
+int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const uint8_t id[UFC_COMM_ID_BYTES]);
+int ufc_comm_destroy(ufc_comm* comm);
+/* Last RCCL result code seen by this communicator (0 if none). */
+int ufc_comm_last_error(const ufc_comm* comm);
+/* Collective: the batched gate on this rank's shard, then the gather to `root`.
+ *   d_frames     this rank's shard (frame k of the shard at d_frames + k * stride, stride >= frame_len)
+ *   d_crc_out    root: n_total words in global frame order; other ranks: their shard's words
+ *   d_valid_out  likewise, bytes; either output may be NULL, identically on every rank
+ *   stream       the gate runs here (the root's own shard is complete when it is)
+ *   gather_stream  the RCCL transfers run here, each chunk of the shard after its gate, so that the
+ *                transfer of one chunk overlaps the gate of the next; NULL = `stream`.  The root's
+ *                output is complete once both streams are; a sender's output may be rewritten
+ *                once gather_stream has passed this call.
+ * One host thread per communicator at a time; every rank must make the same calls in the same
+ * order with the same n_total, frame_len and root. */
+int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size_t frame_len, uint64_t n_total,
+                    uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream);
 
 #ifdef __cplusplus
 }

@@ -36,6 +36,9 @@ def lib():
             "ufo_seal_fixed": (None, [vp, sz, sz, sz]),
             "ufo_seal_varlen": (None, [vp, vp, sz]),
             "ufo_validate_fixed_mt": (ctypes.c_int, [vp, sz, sz, sz, vp, vp, ctypes.c_int]),
+            "ufo_validate_varlen_mt": (ctypes.c_int, [vp, vp, sz, vp, vp, ctypes.c_int]),
+            "ufo_seal_fixed_mt": (ctypes.c_int, [vp, sz, sz, sz, ctypes.c_int]),
+            "ufo_seal_varlen_mt": (ctypes.c_int, [vp, vp, sz, ctypes.c_int]),
             "ufo_write_handshake_syn": (sz, [vp, u8, u32, u32, u32, u32]),
             "ufo_write_handshake_syn_ack": (sz, [vp, u32, u32, u32, u32, u32]),
             "ufo_write_handshake_ack": (sz, [vp, u32]),
@@ -113,6 +116,37 @@ def validate_fixed_mt(frames: np.ndarray, stride, frame_len, n, nthreads):
     if rc != 0:
         raise RuntimeError("ufo_validate_fixed_mt failed")
     return crc, valid
+
+
+def default_threads():
+    """Host threads for the full-size checks: the CPUs this process may run on (the GPU box's
+    share; os.cpu_count() there reports the whole machine), capped at 64."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(64, n))
+
+
+def validate_varlen_mt(data: np.ndarray, offsets: np.ndarray, nthreads=None):
+    data = np.ascontiguousarray(data, dtype=np.uint8)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    n = offsets.size - 1
+    crc = np.zeros(n, dtype=np.uint32)
+    valid = np.zeros(n, dtype=np.uint8)
+    lib().ufo_validate_varlen_mt(_p(data), _p(offsets), n, _p(crc), _p(valid), int(nthreads or default_threads()))
+    return crc, valid
+
+
+def seal_fixed_mt(frames: np.ndarray, stride, frame_len, n, nthreads=None):
+    assert frames.dtype == np.uint8 and frames.flags.c_contiguous
+    lib().ufo_seal_fixed_mt(_p(frames), stride, frame_len, n, int(nthreads or default_threads()))
+
+
+def seal_varlen_mt(data: np.ndarray, offsets: np.ndarray, nthreads=None):
+    assert data.dtype == np.uint8 and data.flags.c_contiguous
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lib().ufo_seal_varlen_mt(_p(data), _p(offsets), offsets.size - 1, int(nthreads or default_threads()))
 
 
 def validate_varlen(data: np.ndarray, offsets: np.ndarray):

@@ -42,6 +42,26 @@ def _p16(v):
     return bytes(((v >> 8) & 0xFF, v & 0xFF))
 
 
+MAX_FRAGMENT_SIZE = MAX_FRAME_SIZE - 10 - 14  # src/lib.rs:297 (DATA_FRAME_OVERHEAD, MAX_DATAGRAM_OVERHEAD)
+
+
+def datagram_is_valid(dg):
+    """src/half_connection/packet_receiver/mod.rs:12-30, the receive side's check of a decoded
+    datagram before it enters the reassembly window (handle_datagram, :147-150)."""
+    if dg["channel_id"] >= MAX_CHANNELS:  # CHANNEL_COUNT = MAX_CHANNELS (src/lib.rs:278)
+        return False
+    if dg["channel_parent_lead"] != 0:
+        if dg["window_parent_lead"] == 0 or dg["channel_parent_lead"] < dg["window_parent_lead"]:
+            return False
+    if dg["fragment_id"] > dg["fragment_id_last"]:
+        return False
+    if dg["fragment_id"] < dg["fragment_id_last"] and len(dg["data"]) != MAX_FRAGMENT_SIZE:
+        return False
+    if len(dg["data"]) > MAX_FRAGMENT_SIZE:
+        return False
+    return True
+
+
 # ---- decode (serial/mod.rs:54-434, 674-706) ----
 
 def read_datagram(d):
@@ -252,6 +272,23 @@ def random_data_frame(rng: random.Random, max_datagrams=64, max_data=100):
             dgs.append(dict(sequence_id=seq, channel_id=ch, window_parent_lead=rng.getrandbits(16),
                             channel_parent_lead=rng.getrandbits(16), fragment_id=a, fragment_id_last=b,
                             data=data(0, max_data)))
+    return {"kind": "data", "sequence_id": rng.getrandbits(32), "nonce": bool(rng.getrandbits(1)), "datagrams": dgs}
+
+
+def receive_side_data_frame(rng: random.Random, max_datagrams=6):
+    """A data frame whose datagrams cover every branch of datagram_is_valid
+    (packet_receiver/mod.rs:12-30): parent leads zero / equal / below / above, fragment ids in and
+    out of order, fragments of exactly MAX_FRAGMENT_SIZE bytes or not, payloads over it."""
+    dgs = []
+    for _ in range(1 + rng.randrange(max_datagrams)):
+        w = rng.choice([0, 1, rng.randrange(1, 300), rng.getrandbits(16)])
+        c = rng.choice([0, w, max(w - 1, 0), w + 1, rng.getrandbits(16)]) & 0xFFFF
+        a = rng.choice([0, 1, rng.getrandbits(16)])
+        b = rng.choice([a, a + 1, max(a - 1, 0), rng.getrandbits(16)]) & 0xFFFF
+        n = rng.choice([0, 5, MAX_FRAGMENT_SIZE - 1, MAX_FRAGMENT_SIZE, MAX_FRAGMENT_SIZE + 1, rng.randrange(300)])
+        dgs.append(dict(sequence_id=rng.getrandbits(20), channel_id=rng.randrange(MAX_CHANNELS), window_parent_lead=w,
+                        channel_parent_lead=c, fragment_id=a, fragment_id_last=b,
+                        data=bytes(rng.getrandbits(8) for _ in range(n))))
     return {"kind": "data", "sequence_id": rng.getrandbits(32), "nonce": bool(rng.getrandbits(1)), "datagrams": dgs}
 
 

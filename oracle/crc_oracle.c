@@ -155,11 +155,72 @@ int ufo_validate_fixed_mt(const uint8_t* frames, size_t stride, size_t frame_len
     jobs[t].lo = n * (size_t)t / (size_t)nthreads; jobs[t].hi = n * (size_t)(t + 1) / (size_t)nthreads;
     jobs[t].crc_out = crc_out; jobs[t].valid_out = valid_out;
   }
-  for (int t = 1; t < nthreads; t++)
-    if (pthread_create(&th[t], NULL, ufo_worker, &jobs[t]) != 0) return -1;
+  int started = 1;
+  for (int t = 1; t < nthreads; t++, started++)
+    if (pthread_create(&th[t], NULL, ufo_worker, &jobs[t]) != 0) break;
   ufo_worker(&jobs[0]);
-  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  for (int t = 1; t < started; t++) pthread_join(th[t], NULL);
+  for (int t = started; t < nthreads; t++) ufo_worker(&jobs[t]);
   return 0;
+}
+
+/* The same loops over a CSR batch and the seals, frames partitioned contiguously over
+ * `nthreads` pthreads (full-size parity checks in tests/ and the config-3 CPU baseline). */
+typedef struct {
+  int op; /* 0 validate varlen, 1 seal fixed, 2 seal varlen */
+  uint8_t* bytes; const uint64_t* offsets; size_t stride, frame_len, lo, hi;
+  uint32_t* crc_out; uint8_t* valid_out;
+} ufo_job2;
+
+static void* ufo_worker2(void* p) {
+  ufo_job2* j = (ufo_job2*)p;
+  if (j->op == 0) {
+    ufo_validate_varlen(j->bytes, j->offsets + j->lo, j->hi - j->lo, j->crc_out ? j->crc_out + j->lo : NULL,
+                        j->valid_out ? j->valid_out + j->lo : NULL);
+  } else if (j->op == 1) {
+    ufo_seal_fixed(j->bytes + j->lo * j->stride, j->stride, j->frame_len, j->hi - j->lo);
+  } else {
+    ufo_seal_varlen(j->bytes, j->offsets + j->lo, j->hi - j->lo);
+  }
+  return NULL;
+}
+
+static int ufo_run2(ufo_job2 proto, size_t n, int nthreads) {
+  ensure_table();
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  ufo_job2 jobs[256];
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t] = proto;
+    jobs[t].lo = n * (size_t)t / (size_t)nthreads;
+    jobs[t].hi = n * (size_t)(t + 1) / (size_t)nthreads;
+  }
+  int started = 1;
+  for (int t = 1; t < nthreads; t++, started++)
+    if (pthread_create(&th[t], NULL, ufo_worker2, &jobs[t]) != 0) break;
+  ufo_worker2(&jobs[0]);
+  for (int t = 1; t < started; t++) pthread_join(th[t], NULL);
+  if (started != nthreads) { /* finish the ranges whose thread did not start */
+    for (int t = started; t < nthreads; t++) ufo_worker2(&jobs[t]);
+  }
+  return 0;
+}
+
+int ufo_validate_varlen_mt(const uint8_t* bytes, const uint64_t* offsets, size_t n, uint32_t* crc_out,
+                           uint8_t* valid_out, int nthreads) {
+  ufo_job2 j = {0, (uint8_t*)bytes, offsets, 0, 0, 0, 0, crc_out, valid_out};
+  return ufo_run2(j, n, nthreads);
+}
+
+int ufo_seal_fixed_mt(uint8_t* frames, size_t stride, size_t frame_len, size_t n, int nthreads) {
+  ufo_job2 j = {1, frames, NULL, stride, frame_len, 0, 0, NULL, NULL};
+  return ufo_run2(j, n, nthreads);
+}
+
+int ufo_seal_varlen_mt(uint8_t* bytes, const uint64_t* offsets, size_t n, int nthreads) {
+  ufo_job2 j = {2, bytes, offsets, 0, 0, 0, 0, NULL, NULL};
+  return ufo_run2(j, n, nthreads);
 }
 
 /* ---------------------------------------------------------------------------------------

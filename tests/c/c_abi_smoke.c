@@ -62,6 +62,23 @@ int main(void) {
   if (ufc_device_count() == 0) CHECK(rc == UFC_ERR_NO_DEVICE && ctx == NULL);
   if (ctx) ufc_ctx_destroy(ctx);
   CHECK(ufc_error_string(UFC_ERR_INVALID_ARG) != NULL);
+  CHECK(ufc_error_string(UFC_ERR_COMM) != NULL);
+
+  /* NULL buffers are argument errors, never crashes (no context here either way) */
+  uint32_t scratch[4];
+  CHECK(ufc_seal_host_slots(NULL, NULL, 1472, NULL, 4, scratch) == UFC_ERR_INVALID_ARG);
+  CHECK(ufc_seal_host_varlen(NULL, NULL, NULL, 4, scratch) == UFC_ERR_INVALID_ARG);
+  CHECK(ufc_ctx_set_option(NULL, UFC_OPT_FIXED_KERNEL, UFC_FIXED_AUTO) == UFC_ERR_INVALID_ARG);
+
+  /* multi-GPU layout: config 4 (100M frames over 8 GPUs) -> 12.5M frames per rank, 3 chunks */
+  uint64_t first = 0, count = 0;
+  CHECK(ufc_shard_range(100000000u, 8, 3, &first, &count) == UFC_OK && first == 37500000u && count == 12500000u);
+  CHECK(ufc_shard_chunk(100000000u, 8, 3, 2, &first, &count) == 3 && first + count == 50000000u);
+  CHECK(ufc_shard_range(10, 2, 2, &first, &count) == UFC_ERR_INVALID_ARG);
+  ufc_comm* comm = NULL;
+  uint8_t id[UFC_COMM_ID_BYTES] = {0};
+  CHECK(ufc_comm_create(&comm, NULL, 2, 0, id) == UFC_ERR_INVALID_ARG && comm == NULL);
+  CHECK(ufc_crc_sharded(NULL, NULL, 1500, 1500, 10, NULL, NULL, 0, NULL, NULL) == UFC_ERR_INVALID_ARG);
 
   if (fails) return 1;
   printf("c abi ok\n");

@@ -236,3 +236,40 @@ def test_parse_batch_host_vs_oracle(threads, with_valid):
         assert bool(info["crc_ok"]) == bool(oracle.frame_validate(fb)[0])
         first += cnt
     assert first == items.size
+
+
+def test_datagram_is_valid_vs_oracle():
+    """ufc_datagram_is_valid and the parses' UFC_ITEM_VALID flag == the restated
+    datagram_is_valid (src/half_connection/packet_receiver/mod.rs:12-30) on datagrams that cover
+    each of its branches, decoded by the host batch parse."""
+    rng = random.Random(1230)
+    frames = [C.frame_write(C.receive_side_data_frame(rng)) for _ in range(400)]
+    offsets = np.zeros(len(frames) + 1, dtype=np.uint64)
+    offsets[1:] = np.cumsum([len(f) for f in frames])
+    data = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
+    infos, items = F.parse_batch_host(data, offsets)
+    seen = {True: 0, False: 0}
+    for i, fb in enumerate(frames):
+        ref = C.frame_read(fb)
+        assert infos[i]["ok"] and ref is not None
+        first, cnt = int(infos[i]["item_first"]), int(infos[i]["item_count"])
+        for it, dg in zip(items[first:first + cnt], ref["datagrams"]):
+            want = C.datagram_is_valid(dg)
+            assert bool(it["flags"] & 1) == want
+            d = F.Datagram(dg["sequence_id"], dg["channel_id"], dg["window_parent_lead"], dg["channel_parent_lead"],
+                           dg["fragment_id"], dg["fragment_id_last"], dg["data"])
+            assert F.datagram_is_valid(d) == want
+            seen[want] += 1
+    assert seen[True] > 100 and seen[False] > 100, seen
+    # each rule alone (packet_receiver/mod.rs:13-29)
+    ok = dict(sequence_id=1, channel_id=3, window_parent_lead=5, channel_parent_lead=7, fragment_id=0,
+              fragment_id_last=0, data=b"x" * 10)
+    for change, want in [({}, True), ({"channel_parent_lead": 0, "window_parent_lead": 0}, True),
+                         ({"window_parent_lead": 0}, False), ({"channel_parent_lead": 4}, False),
+                         ({"channel_parent_lead": 5}, True), ({"fragment_id": 2, "fragment_id_last": 1}, False),
+                         ({"fragment_id": 1, "fragment_id_last": 2}, False),
+                         ({"fragment_id": 1, "fragment_id_last": 2, "data": b"y" * 1448}, True),
+                         ({"data": b"z" * 1448}, True), ({"data": b"z" * 1449}, False)]:
+        dg = dict(ok, **change)
+        assert C.datagram_is_valid(dg) == want, change
+        assert F.datagram_is_valid(F.Datagram(**dg)) == want, change

@@ -1,0 +1,217 @@
+"""GPU parity at BASELINE.json's full sizes, every frame compared bit-exact with the CPU oracle
+(oracle/crc_oracle.c: crc.rs:94-104 and the gate of serial/mod.rs:675-690), plus the committed
+golden fixtures run straight through the HIP path.
+
+  config 2   1M x 1500-B frames generated on the host, sealed by the oracle, one bit flipped in
+             every 1000th frame; the GPU gate vs the oracle; the GPU seal of the zero-trailer
+             frames vs the oracle's seal (byte-identical batch).
+  config 3   10M frames, lengths U[64,1500] (seed 0x5EED0002), sealed by the GPU, every 997th
+             frame flipped; the oracle re-validates every frame (so it checks the GPU seal too) and
+             its CRC words must equal the GPU gate's.
+  config 4   one GPU's shard of the 100M-frame batch: frames [37.5M, 50M) (rank 3 of 8) of seed
+             0x5EED0003, 18.75 GB, sealed on the GPU, every 1000th frame flipped; as config 3.
+The oracle runs multithreaded over the whole batch (16 threads: the GPU box's CPU share).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from uflow_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+THREADS = 16
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _host(t):
+    return t.cpu().numpy()
+
+
+def _compare(crc_d, valid_d, ref_crc, ref_valid, what):
+    got_crc = _host(crc_d).view(np.uint32)
+    got_valid = _host(valid_d)
+    bad = np.nonzero(got_crc != ref_crc)[0]
+    assert bad.size == 0, f"{what}: {bad.size} CRC mismatches, first frames {bad[:8]}"
+    bad = np.nonzero(got_valid != ref_valid)[0]
+    assert bad.size == 0, f"{what}: {bad.size} valid-flag mismatches, first frames {bad[:8]}"
+
+
+def test_config2_full_batch(engine):
+    n, L = 1_000_000, 1500
+    rng = np.random.default_rng(synth.SEED_CONFIG2)
+    host = rng.integers(0, 256, size=n * L, dtype=np.uint8)
+    zero_trailers = host.copy()
+    zero_trailers.reshape(n, L)[:, L - 4:] = 0
+    oracle.seal_fixed_mt(host, L, L, n, THREADS)
+    flipped = np.arange(0, n, 1000)
+    host[flipped * L + 17] ^= 0x04
+    ref_crc, ref_valid = oracle.validate_fixed_mt(host, L, L, n, THREADS)
+    assert int(ref_valid.sum()) == n - flipped.size
+    d = torch.from_numpy(host).to(DEV)
+    crc, valid = engine.crc_fixed(d, L, n=n)
+    torch.cuda.synchronize()
+    _compare(crc, valid, ref_crc, ref_valid, "config 2 gate")
+    # the encode side: GPU seal of the zero-trailer batch == the oracle's seal, byte for byte
+    host[flipped * L + 17] ^= 0x04
+    z = torch.from_numpy(zero_trailers).to(DEV)
+    crc_out = torch.empty(n, dtype=torch.int32, device=DEV)
+    engine.seal_fixed(z, L, n=n, crc_out=crc_out)
+    torch.cuda.synchronize()
+    assert torch.equal(z, torch.from_numpy(host).to(DEV)), "config 2 seal differs from the oracle's"
+    assert np.array_equal(_host(crc_out).view(np.uint32),
+                          oracle.validate_fixed_mt(host, L, L, n, THREADS)[0])
+
+
+def test_config3_full_batch(engine):
+    n = 10_000_000
+    data, offsets = synth.varlen_batch(n, 64, 1500, synth.SEED_CONFIG3, device=DEV)
+    engine.seal_varlen(data, offsets)
+    flipped = torch.arange(0, n, 997, device=DEV)
+    synth.flip_bits(data, offsets[flipped], byte_in_frame=7, mask=0x20)
+    crc, valid = engine.crc_varlen(data, offsets)
+    torch.cuda.synchronize()
+    h_data, h_off = _host(data), _host(offsets).astype(np.uint64)
+    ref_crc, ref_valid = oracle.validate_varlen_mt(h_data, h_off, THREADS)
+    expect = np.ones(n, np.uint8)
+    expect[_host(flipped)] = 0
+    assert np.array_equal(ref_valid, expect), "the GPU seal left frames the oracle rejects"
+    _compare(crc, valid, ref_crc, ref_valid, "config 3 gate")
+
+
+def test_config4_shard_full(engine):
+    world, rank, total, L = 8, 3, 100_000_000, 1500
+    lo, hi = total * rank // world, total * (rank + 1) // world
+    n = hi - lo
+    frames = synth.fixed_frames(n, L, synth.SEED_CONFIG4, first_frame=lo, device=DEV)
+    engine.seal_fixed(frames, L, n=n)
+    flipped = torch.arange(0, n, 1000, device=DEV)
+    synth.flip_bits(frames, flipped * L)
+    crc, valid = engine.crc_fixed(frames, L, n=n)
+    torch.cuda.synchronize()
+    host = _host(frames)
+    del frames
+    torch.cuda.empty_cache()
+    ref_crc, ref_valid = oracle.validate_fixed_mt(host, L, L, n, THREADS)
+    expect = np.ones(n, np.uint8)
+    expect[_host(flipped)] = 0
+    assert np.array_equal(ref_valid, expect), "the GPU seal left frames the oracle rejects"
+    _compare(crc, valid, ref_crc, ref_valid, "config 4 shard gate")
+
+
+# ---- the committed golden fixtures, straight through the HIP path ----
+
+def _csr(frames):
+    offsets = np.zeros(len(frames) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum([len(f) for f in frames])
+    return np.frombuffer(b"".join(frames), dtype=np.uint8).copy(), offsets
+
+
+def _gpu_varlen(engine, data, offsets):
+    crc, valid = engine.crc_varlen(torch.from_numpy(data).to(DEV), torch.from_numpy(offsets.astype(np.int64)).to(DEV))
+    torch.cuda.synchronize()
+    return _host(crc).view(np.uint32), _host(valid)
+
+
+def _gpu_seal_varlen(engine, data, offsets):
+    d = torch.from_numpy(data.copy()).to(DEV)
+    crc_out = torch.empty(offsets.size - 1, dtype=torch.int32, device=DEV)
+    engine.seal_varlen(d, torch.from_numpy(offsets.astype(np.int64)).to(DEV), crc_out=crc_out)
+    torch.cuda.synchronize()
+    return _host(d), _host(crc_out).view(np.uint32)
+
+
+def test_golden_random_frames_fixture(engine):
+    """tests/golden/random_frames.npz: 120 frames of 0..1600 B, every 7th bit-flipped."""
+    z = np.load(os.path.join(GOLDEN, "random_frames.npz"))
+    crc, valid = _gpu_varlen(engine, z["data"], z["offsets"])
+    assert np.array_equal(crc, z["crc"])
+    assert np.array_equal(valid, z["valid"])
+
+
+def test_golden_crc_ramp_fixture(engine):
+    """tests/golden/crc_lengths.json: crc(bytes(i % 256 for i in range(n))) for n = 0..300 and the
+    constant patterns, as frames body + BE trailer: the GPU gate returns the fixture CRC and accepts
+    every frame of >= 5 bytes; the GPU seal of the zero-trailer frames writes the fixture CRC."""
+    with open(os.path.join(GOLDEN, "crc_lengths.json")) as f:
+        g = json.load(f)
+    bodies = [(bytes(i % 256 for i in range(n)), int(c, 16)) for n, c in g["ramp"]]
+    pat = g["patterns"]
+    bodies += [(b"\x00" * 1500, int(pat["zeros_1500"], 16)), (b"\xff" * 1500, int(pat["ones_1500"], 16)),
+               (b"\xa5" * 1472, int(pat["a5_1472"], 16)), (b"123456789", int(pat["ascii_123456789"], 16))]
+    frames = [b + c.to_bytes(4, "big") for b, c in bodies]
+    data, offsets = _csr(frames)
+    crc, valid = _gpu_varlen(engine, data, offsets)
+    assert [int(x) for x in crc] == [c for _, c in bodies]
+    assert [int(v) for v in valid] == [1 if len(f) >= 5 else 0 for f in frames]
+    zeroed = data.copy()
+    for i in range(len(frames)):
+        zeroed[offsets[i + 1] - 4:offsets[i + 1]] = 0
+    sealed, seal_crc = _gpu_seal_varlen(engine, zeroed, offsets)
+    assert np.array_equal(sealed, data)
+    assert [int(x) for x in seal_crc] == [c for _, c in bodies]
+    # the same bodies of one length as a fixed-stride batch (lean / generic fixed kernels)
+    for n in (1, 5, 251, 252, 253, 300):
+        fr = frames[n]
+        batch = np.frombuffer(fr * 4099, dtype=np.uint8).copy()
+        c, v = engine.crc_fixed(torch.from_numpy(batch).to(DEV), len(fr), n=4099)
+        torch.cuda.synchronize()
+        assert set(_host(c).view(np.uint32).tolist()) == {bodies[n][1]}
+        assert set(_host(v).tolist()) == {1 if len(fr) >= 5 else 0}
+
+
+def test_golden_reference_frames_fixture(engine):
+    """tests/golden/frames.json: the reference tests' fixed-value frames (serial/mod.rs:760-925),
+    gated and sealed on the GPU; their truncations (serial/mod.rs:751-758) and one extra byte
+    (:738-749) are rejected."""
+    with open(os.path.join(GOLDEN, "frames.json")) as f:
+        fx = json.load(f)["frames"]
+    frames = [bytes.fromhex(x["hex"]) for x in fx]
+    data, offsets = _csr(frames)
+    crc, valid = _gpu_varlen(engine, data, offsets)
+    assert [int(c) for c in crc] == [int(x["crc"], 16) for x in fx]
+    assert valid.tolist() == [x["valid"] for x in fx]
+    zeroed = data.copy()
+    for i in range(len(frames)):
+        zeroed[offsets[i + 1] - 4:offsets[i + 1]] = 0
+    sealed, _ = _gpu_seal_varlen(engine, zeroed, offsets)
+    assert np.array_equal(sealed, data)
+    bad = [fr[:k] for fr in frames for k in range(len(fr))] + [fr + b"\x00" for fr in frames]
+    d2, o2 = _csr(bad)
+    _, v2 = _gpu_varlen(engine, d2, o2)
+    assert not v2.any()
+
+
+def test_parse_datagram_validity_flags(engine):
+    """The GPU parse's UFC_ITEM_VALID flags == datagram_is_valid (packet_receiver/mod.rs:12-30) of
+    the oracle's decode, on datagrams covering every branch of the check."""
+    import random
+    from oracle import codec as C
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE
+    rng = random.Random(4321)
+    frames = [C.frame_write(C.receive_side_data_frame(rng)) for _ in range(3000)]
+    data, offsets = _csr(frames)
+    d = torch.from_numpy(data).to(DEV)
+    o = torch.from_numpy(offsets).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    infos = _host(infos).view(FRAME_INFO_DTYPE).reshape(-1)
+    items = _host(items).view(ITEM_DTYPE).reshape(-1)
+    k = 0
+    counts = {True: 0, False: 0}
+    for i, fb in enumerate(frames):
+        ref = C.frame_read(fb)
+        assert infos[i]["ok"] == 1 and int(infos[i]["item_first"]) == k
+        for it, dg in zip(items[k:k + int(infos[i]["item_count"])], ref["datagrams"]):
+            want = C.datagram_is_valid(dg)
+            assert bool(it["flags"] & 1) == want, (i, dg)
+            counts[want] += 1
+        k += int(infos[i]["item_count"])
+    assert int(_host(used)[0]) == k
+    assert counts[True] > 1000 and counts[False] > 1000, counts

@@ -392,19 +392,59 @@ def test_fixed_multi_launch(engine, frame_len, extra):
         assert np.array_equal(got, ref_crc)
 
 
-@pytest.mark.parametrize("cfg", [{"UFC_VL_SORT": "1"}, {"UFC_VL_CFG": "blocked8"}])
-def test_varlen_alternate_modes(engine, monkeypatch, cfg):
-    """The varlen kernel's A/B modes (read at launch time): run-sorted records, and the static
-    blocked schedule at 8 waves -- mixed lengths, edge lengths, seal, gapped pairs."""
-    for k, v in cfg.items():
-        monkeypatch.setenv(k, v)
-    rng = np.random.default_rng(91)
-    _varlen_case(engine, rng, rng.integers(64, 1501, size=20_003).tolist(), flip_every=97)
-    lens = [0, 1, 2, 3, 4, 5, 6, 255, 256, 257, 258, 259, 260, 1472, 8192, 0, 9, 3000, 1, 1532, 1533] * 9
-    rng.shuffle(lens)
-    _varlen_case(engine, rng, lens, seal=False)
-    test_seal_varlen(engine)
-    test_pairs_gapped_layout(engine)
+@pytest.mark.parametrize("mode", ["sorted", "blocked8", "generic"])
+def test_varlen_alternate_modes(engine, mode):
+    """The varlen kernel's A/B modes (ufc_ctx_set_option): run-sorted records, the static blocked
+    schedule at 8 waves, the generic kernel -- mixed lengths, edge lengths, seal, gapped pairs."""
+    from uflow_amd import _native as N
+    value = {"sorted": N.UFC_VARLEN_SORTED, "blocked8": N.UFC_VARLEN_BLOCKED8, "generic": N.UFC_VARLEN_GENERIC}[mode]
+    engine.set_option(N.UFC_OPT_VARLEN_KERNEL, value)
+    try:
+        assert engine.get_option(N.UFC_OPT_VARLEN_KERNEL) == value
+        rng = np.random.default_rng(91)
+        _varlen_case(engine, rng, rng.integers(64, 1501, size=20_003).tolist(), flip_every=97)
+        lens = [0, 1, 2, 3, 4, 5, 6, 255, 256, 257, 258, 259, 260, 1472, 8192, 0, 9, 3000, 1, 1532, 1533] * 9
+        rng.shuffle(lens)
+        _varlen_case(engine, rng, lens, seal=False)
+        test_seal_varlen(engine)
+        if mode != "generic":  # (pairs: lean kernel only)
+            test_pairs_gapped_layout(engine)
+    finally:
+        engine.set_option(N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_AUTO)
+
+
+@pytest.mark.parametrize("mode", ["generic", "claim16"])
+def test_fixed_alternate_modes(engine, mode):
+    from uflow_amd import _native as N
+    value = {"generic": N.UFC_FIXED_GENERIC, "claim16": N.UFC_FIXED_CLAIM16}[mode]
+    engine.set_option(N.UFC_OPT_FIXED_KERNEL, value)
+    try:
+        rng = np.random.default_rng(92)
+        for frame_len in (64, 1472, 1500):
+            _fixed_case(engine, rng, frame_len, frame_len, 9_999, flip_every=13)
+    finally:
+        engine.set_option(N.UFC_OPT_FIXED_KERNEL, N.UFC_FIXED_AUTO)
+
+
+def test_parse_two_streams(engine):
+    """Two batch parses queued on different streams of one context at once: each stream has its own
+    scan scratch, so both results equal the single-stream parse."""
+    frames, data, offsets = _codec_batch(11, 2000)
+    d = torch.from_numpy(data).to(DEV)
+    o = torch.from_numpy(offsets).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    torch.cuda.synchronize()
+    ref = [t.cpu() for t in engine.parse_varlen(d, o, valid)]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    outs = []
+    for _ in range(3):
+        for s in (s1, s2):
+            with torch.cuda.stream(s):
+                outs.append(engine.parse_varlen(d, o, valid, stream=s))
+    torch.cuda.synchronize()
+    for got in outs:
+        for a, b in zip(got, ref):
+            assert torch.equal(a.cpu(), b)
 
 
 def test_fixed_random_shapes(engine):

@@ -138,3 +138,69 @@ def test_c_caller_links_and_runs(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     assert "c abi ok" in r.stdout
+
+
+def _unbound_engine():
+    """A FrameCrcEngine with no device context (CPU): argument checks run before any C-ABI call."""
+    import torch
+    from uflow_amd.batch import FrameCrcEngine
+    eng = FrameCrcEngine.__new__(FrameCrcEngine)
+    eng.device = torch.device("cpu")
+    eng._ctx = ctypes.c_void_p()
+    return eng
+
+
+def test_batch_wrappers_reject_bad_tensors():
+    """batch.py checks dtype and size of every tensor before the kernels see its pointer (a short
+    crc_out or a non-uint8 frames tensor would otherwise be written or read out of bounds)."""
+    import torch
+    eng = _unbound_engine()
+    frames = torch.zeros(10 * 100, dtype=torch.uint8)
+    with pytest.raises(ValueError, match="crc_out"):
+        eng.crc_fixed(frames, 100, n=10, crc_out=torch.zeros(9, dtype=torch.int32))
+    with pytest.raises(ValueError, match="crc_out"):
+        eng.crc_fixed(frames, 100, n=10, crc_out=torch.zeros(10, dtype=torch.int16))
+    with pytest.raises(ValueError, match="valid_out"):
+        eng.crc_fixed(frames, 100, n=10, valid_out=torch.zeros(10, dtype=torch.int32))
+    with pytest.raises(ValueError, match="valid_out"):
+        eng.crc_fixed(frames, 100, n=10, valid_out=torch.zeros(5, dtype=torch.uint8))
+    with pytest.raises(ValueError, match="frames"):
+        eng.crc_fixed(frames.view(torch.int32), 100, n=10)
+    with pytest.raises(ValueError, match="frames"):
+        eng.crc_fixed(frames, 100, n=11)
+    with pytest.raises(ValueError, match="frames"):
+        eng.seal_fixed(frames, 100, stride=101, n=10)
+    offsets = torch.arange(0, 1001, 100, dtype=torch.int64)
+    with pytest.raises(ValueError, match="offsets"):
+        eng.crc_varlen(frames, offsets.to(torch.int32))
+    with pytest.raises(ValueError, match="crc_out"):
+        eng.crc_varlen(frames, offsets, crc_out=torch.zeros(3, dtype=torch.int32))
+    with pytest.raises(ValueError, match="data"):
+        eng.seal_varlen(frames.view(torch.int16), offsets)
+    with pytest.raises(ValueError, match="pairs"):
+        eng.crc_pairs(frames, torch.zeros(10, dtype=torch.int64))
+    with pytest.raises(ValueError, match="pairs"):
+        eng.crc_pairs(frames, torch.zeros((10, 2), dtype=torch.int32))
+    with pytest.raises(ValueError, match="valid"):
+        eng.parse_varlen(frames, offsets, torch.zeros(4, dtype=torch.uint8))
+    # well-formed arguments reach the C ABI, which refuses the missing context (no CPU fallback)
+    from uflow_amd._native import NativeError
+    import types
+    with pytest.raises(NativeError):
+        eng.crc_fixed(frames, 100, n=10, stream=types.SimpleNamespace(cuda_stream=0))
+
+
+def test_ctx_options_reject_without_context():
+    l = _native.lib()
+    null = ctypes.c_void_p()
+    assert l.ufc_ctx_set_option(null, _native.UFC_OPT_FIXED_KERNEL, 0) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_ctx_get_option(null, 0) == _native.UFC_ERR_INVALID_ARG
+
+
+def test_seal_host_entry_points_reject_null_buffers():
+    l = _native.lib()
+    null = ctypes.c_void_p()
+    scratch = (ctypes.c_uint32 * 4)()
+    # no context: invalid argument (never a crash); zero frames: nothing to do
+    assert l.ufc_seal_host_slots(null, None, 1472, None, 4, scratch) == _native.UFC_ERR_INVALID_ARG
+    assert l.ufc_seal_host_varlen(null, None, None, 4, scratch) == _native.UFC_ERR_INVALID_ARG

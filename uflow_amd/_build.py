@@ -11,9 +11,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libuflowcrc.so")
-SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_parse.hip", "ufc_api.cpp", "crc_math.cpp",
+SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_parse.hip", "ufc_api.cpp", "ufc_shard.cpp", "crc_math.cpp",
            "frame_codec.cpp"]
-HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp", "frame_codec_core.hpp", "frame_parse.hpp"]
+HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp", "frame_codec_core.hpp", "frame_parse.hpp",
+           "ufc_internal.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
@@ -34,16 +35,36 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
         return target
     # No atomic optimizer: the lean kernel's single-lane claim atomics must stay plain
     # global_atomic_add (the optimizer reads the result back at once, forcing a vmcnt(0) wait).
-    cmd = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-shared", "-std=c++17", "-Wall",
-           "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-           "-o", target + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    flags = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall",
+             "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
     if tuning:
-        cmd.insert(1, "-DUFC_TUNING")
-    for d in defines:
-        cmd.insert(1, "-D" + d)
+        flags.append("-DUFC_TUNING")
+    flags += ["-D" + d for d in defines]
+    # One object per source, compiled in parallel, then one link.
+    objdir = os.path.join(REPO_DIR, "build", "obj_" + os.path.basename(target).replace(".", "_"))
+    os.makedirs(objdir, exist_ok=True)
+    jobs, objs = [], []
+    hdrs = deps[len(SOURCES):]
+    for src in SOURCES:
+        obj = os.path.join(objdir, src + ".o")
+        objs.append(obj)
+        if force or _stale(obj, [os.path.join(CSRC, src)] + hdrs + [__file__]):
+            jobs.append(flags + ["-c", os.path.join(CSRC, src), "-o", obj])
+    from concurrent.futures import ThreadPoolExecutor
+
+    def run(cmd):
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        return subprocess.run(cmd).returncode
+
+    with ThreadPoolExecutor(max_workers=max(1, min(8, len(jobs)))) as ex:
+        rcs = list(ex.map(run, jobs))
+    if any(rcs):
+        raise subprocess.CalledProcessError(max(rcs), "hipcc")
+    link = [HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", target + ".tmp"] + objs + ["-ldl"]
     if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+        print(" ".join(link), file=sys.stderr)
+    subprocess.run(link, check=True)
     os.replace(target + ".tmp", target)
     return target
 

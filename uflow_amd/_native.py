@@ -18,6 +18,13 @@ UFC_ERR_INVALID_ARG = -1
 UFC_ERR_NO_DEVICE = -2
 UFC_ERR_HIP = -3
 UFC_ERR_NOMEM = -4
+UFC_ERR_COMM = -5
+UFC_COMM_ID_BYTES = 128
+
+# ufc_ctx_set_option (include/uflow_frame_crc.h)
+UFC_OPT_FIXED_KERNEL, UFC_OPT_VARLEN_KERNEL, UFC_OPT_GENERIC_JC = 0, 1, 2
+UFC_FIXED_AUTO, UFC_FIXED_GENERIC, UFC_FIXED_CLAIM16 = 0, 1, 2
+UFC_VARLEN_AUTO, UFC_VARLEN_GENERIC, UFC_VARLEN_SORTED, UFC_VARLEN_BLOCKED8 = 0, 1, 2, 3
 
 # Every symbol the header declares, with its ctypes signature.
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -31,6 +38,8 @@ _SIGNATURES = {
     "ufc_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "ufc_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "ufc_ctx_last_hip_error": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_ctx_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),
+    "ufc_ctx_get_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ufc_crc_batch_fixed": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                            ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "ufc_crc_batch_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
@@ -49,11 +58,23 @@ _SIGNATURES = {
                                            ctypes.c_size_t, ctypes.c_void_p]),
     "ufc_seal_host_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                             ctypes.c_void_p]),
+    "ufc_shard_range": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint64)]),
+    "ufc_shard_chunk": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "ufc_comm_id_create": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_comm_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_void_p]),
+    "ufc_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_comm_last_error": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_crc_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
+                                       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     # include/uflow_frame_codec.h
     "ufc_frame_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_size_t]),
     "ufc_frame_parse": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p,
                                        ctypes.c_void_p, ctypes.c_size_t]),
+    "ufc_datagram_is_valid": (ctypes.c_int, [ctypes.c_void_p]),
     "ufc_frame_write_fixed": (ctypes.c_size_t, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]),
     "ufc_data_frame_builder_init": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
                                                    ctypes.c_int]),
@@ -83,7 +104,7 @@ class FrameInfo(ctypes.Structure):
 class Item(ctypes.Structure):
     _fields_ = [("id", ctypes.c_uint32), ("channel_id", ctypes.c_uint8), ("form", ctypes.c_uint8),
                 ("window_parent_lead", ctypes.c_uint16), ("channel_parent_lead", ctypes.c_uint16),
-                ("fragment_id", ctypes.c_uint16), ("fragment_id_last", ctypes.c_uint16), ("reserved", ctypes.c_uint16),
+                ("fragment_id", ctypes.c_uint16), ("fragment_id_last", ctypes.c_uint16), ("flags", ctypes.c_uint16),
                 ("data_offset", ctypes.c_uint32), ("data_len", ctypes.c_uint32)]
 
 

@@ -40,6 +40,13 @@ class FrameCrcEngine:
         except Exception:
             pass
 
+    def set_option(self, option, value):
+        """ufc_ctx_set_option (A/B kernel selection; results never depend on it)."""
+        check(lib().ufc_ctx_set_option(self._ctx, int(option), int(value)), "ufc_ctx_set_option")
+
+    def get_option(self, option):
+        return lib().ufc_ctx_get_option(self._ctx, int(option))
+
     def _stream(self, stream):
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         return ctypes.c_void_p(s.cuda_stream)
@@ -48,6 +55,23 @@ class FrameCrcEngine:
         for t in ts:
             if t is not None and (t.device != self.device or not t.is_contiguous()):
                 raise ValueError(f"tensor must be contiguous on {self.device}")
+
+    def _check(self, name, t, dtypes, min_numel):
+        """Device, contiguity, dtype and size of an argument, checked before the C ABI sees its
+        pointer (the kernels trust the sizes they are given)."""
+        if t is None:
+            return
+        if not isinstance(t, torch.Tensor):
+            raise TypeError(f"{name} must be a torch tensor")
+        if t.dtype not in dtypes:
+            raise ValueError(f"{name} must be {' or '.join(str(d) for d in dtypes)}, got {t.dtype}")
+        self._check_dev(t)
+        if t.numel() < min_numel:
+            raise ValueError(f"{name} holds {t.numel()} elements, needs at least {min_numel}")
+
+    def _check_outputs(self, n, crc_out=None, valid_out=None):
+        self._check("crc_out", crc_out, (torch.int32, torch.uint32), n)
+        self._check("valid_out", valid_out, (torch.uint8,), n)
 
     # ---- fixed-stride batches ----
     def crc_fixed(self, frames, frame_len, stride=None, n=None, crc_out=None, valid_out=None,
@@ -60,9 +84,8 @@ class FrameCrcEngine:
             crc_out = torch.empty(n, dtype=torch.int32, device=self.device)
         if valid_out is None and want_valid:
             valid_out = torch.empty(n, dtype=torch.uint8, device=self.device)
-        self._check_dev(frames, crc_out, valid_out)
-        if n and (n - 1) * stride + frame_len > frames.numel():
-            raise ValueError("frames tensor too small for n frames")
+        self._check("frames", frames, (torch.uint8,), (n - 1) * stride + frame_len if n else 0)
+        self._check_outputs(n, crc_out, valid_out)
         check(lib().ufc_crc_batch_fixed(self._ctx, _ptr(frames), stride, frame_len, n, _ptr(crc_out),
                                         _ptr(valid_out), self._stream(stream)), "ufc_crc_batch_fixed")
         return crc_out, valid_out
@@ -71,9 +94,8 @@ class FrameCrcEngine:
         stride = frame_len if stride is None else stride
         if n is None:
             n = (frames.numel() - frame_len) // stride + 1 if frames.numel() >= frame_len else 0
-        self._check_dev(frames, crc_out)
-        if n and (n - 1) * stride + frame_len > frames.numel():
-            raise ValueError("frames tensor too small for n frames")
+        self._check("frames", frames, (torch.uint8,), (n - 1) * stride + frame_len if n else 0)
+        self._check_outputs(n, crc_out)
         check(lib().ufc_seal_batch_fixed(self._ctx, _ptr(frames), stride, frame_len, n, _ptr(crc_out),
                                          self._stream(stream)), "ufc_seal_batch_fixed")
         return crc_out
@@ -87,32 +109,34 @@ class FrameCrcEngine:
             crc_out = torch.empty(max(n, 0), dtype=torch.int32, device=self.device)
         if valid_out is None and want_valid:
             valid_out = torch.empty(max(n, 0), dtype=torch.uint8, device=self.device)
-        if offsets.dtype != torch.int64:
-            raise ValueError("offsets must be int64")
-        self._check_dev(data, offsets, crc_out, valid_out)
+        self._check("offsets", offsets, (torch.int64,), 1)
+        self._check("data", data, (torch.uint8,), 0)
+        self._check_outputs(n, crc_out, valid_out)
         check(lib().ufc_crc_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(crc_out), _ptr(valid_out),
                                          self._stream(stream)), "ufc_crc_batch_varlen")
         return crc_out, valid_out
 
     def seal_varlen(self, data, offsets, crc_out=None, stream=None):
         n = offsets.numel() - 1
-        if offsets.dtype != torch.int64:
-            raise ValueError("offsets must be int64")
-        self._check_dev(data, offsets, crc_out)
+        self._check("offsets", offsets, (torch.int64,), 1)
+        self._check("data", data, (torch.uint8,), 0)
+        self._check_outputs(n, crc_out)
         check(lib().ufc_seal_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(crc_out),
                                           self._stream(stream)), "ufc_seal_batch_varlen")
         return crc_out
 
     def crc_pairs(self, data, pairs, crc_out=None, valid_out=None, stream=None):
         """pairs: int64 tensor [n, 2] of (start, end) byte offsets into data (any gapped layout)."""
+        if pairs.dim() != 2 or pairs.shape[1] != 2:
+            raise ValueError("pairs must have shape [n, 2]")
         n = pairs.shape[0]
-        if pairs.dtype != torch.int64:
-            raise ValueError("pairs must be int64")
         if crc_out is None:
             crc_out = torch.empty(n, dtype=torch.int32, device=self.device)
         if valid_out is None:
             valid_out = torch.empty(n, dtype=torch.uint8, device=self.device)
-        self._check_dev(data, pairs, crc_out, valid_out)
+        self._check("pairs", pairs, (torch.int64,), 2 * n)
+        self._check("data", data, (torch.uint8,), 0)
+        self._check_outputs(n, crc_out, valid_out)
         check(lib().ufc_crc_batch_pairs(self._ctx, _ptr(data), data.numel(), _ptr(pairs), n, _ptr(crc_out),
                                         _ptr(valid_out), self._stream(stream)), "ufc_crc_batch_pairs")
         return crc_out, valid_out
@@ -124,14 +148,14 @@ class FrameCrcEngine:
         the byte rows are ufc_frame_info / ufc_item records (numpy views: uflow_amd.frame
         FRAME_INFO_DTYPE / ITEM_DTYPE).  items_cap defaults to a bound no batch can exceed."""
         n = offsets.numel() - 1
-        if offsets.dtype != torch.int64:
-            raise ValueError("offsets must be int64")
+        self._check("offsets", offsets, (torch.int64,), 1)
+        self._check("data", data, (torch.uint8,), 0)
+        self._check("valid", valid, (torch.uint8,), n)
         if items_cap is None:  # a datagram takes >= 6 bytes, an ack group 9
             items_cap = max(1, data.numel() // 6)
         infos = torch.empty((max(n, 0), 32), dtype=torch.uint8, device=self.device)
         items = torch.empty((items_cap, 24), dtype=torch.uint8, device=self.device)
         used = torch.zeros(1, dtype=torch.int64, device=self.device)
-        self._check_dev(data, offsets, valid, infos, items, used)
         check(lib().ufc_parse_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(valid), _ptr(infos),
                                            _ptr(items), items_cap, _ptr(used), self._stream(stream)),
               "ufc_parse_batch_varlen")

@@ -65,6 +65,11 @@ int ufc_frame_parse(const uint8_t* frame, size_t len, int crc_ok, ufc_frame_info
   return ok ? 1 : 0;
 }
 
+int ufc_datagram_is_valid(const ufc_item* datagram) {  // packet_receiver/mod.rs:12-30
+  if (!datagram) return UFC_ERR_INVALID_ARG;
+  return ufc_codec::datagram_is_valid(*datagram) ? 1 : 0;
+}
+
 size_t ufc_frame_write_fixed(const ufc_frame_info* info, uint8_t* out, size_t cap, int seal) {
   if (!info || !out) return 0;
   size_t len;

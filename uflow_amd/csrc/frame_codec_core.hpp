@@ -30,6 +30,18 @@ UFC_HD uint32_t be16(const Rd& rd, uint32_t i) {
   return (rd(i) << 8) | rd(i + 1);
 }
 
+// src/half_connection/packet_receiver/mod.rs:12-30 `datagram_is_valid` on a decoded datagram
+// (CHANNEL_COUNT = MAX_CHANNELS = 64, src/lib.rs:278; MAX_FRAGMENT_SIZE, src/lib.rs:297).
+UFC_HD bool datagram_is_valid(const ufc_item& d) {
+  if (d.channel_id >= UFC_MAX_CHANNELS) return false;
+  if (d.channel_parent_lead != 0 && (d.window_parent_lead == 0 || d.channel_parent_lead < d.window_parent_lead))
+    return false;
+  if (d.fragment_id > d.fragment_id_last) return false;
+  if (d.fragment_id < d.fragment_id_last && d.data_len != UFC_MAX_FRAGMENT_SIZE) return false;
+  if (d.data_len > UFC_MAX_FRAGMENT_SIZE) return false;
+  return true;
+}
+
 // Parse the payload of a frame of `len` bytes (len >= 5) whose CRC gate passed.  Fills `info`
 // (kind, aux, f[], item_count) and, when items != nullptr, the first `cap` items.  Returns
 // whether Frame::read returns Some.
@@ -111,6 +123,7 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, ufc_
         }
         it.data_offset = 1 + pos + hs;
         it.data_len = dl;
+        it.flags = datagram_is_valid(it) ? UFC_ITEM_VALID : 0;
         if (items && k < cap) items[k] = it;
         pos += hs + dl;
       }

@@ -18,6 +18,7 @@
 #include "crc_math.hpp"
 #include "frame_crc_kernels.hpp"
 #include "frame_parse.hpp"
+#include "ufc_internal.hpp"
 
 struct ufc_ctx {
   int device = -1;
@@ -42,17 +43,51 @@ struct ufc_ctx {
   // concurrent launches on different streams do not share counters (up to kCtrSlots in flight).
   uint32_t* d_ctr = nullptr;
   std::atomic<uint32_t> ctr_seq{0};
-  // Batch parse scratch (item counts, first indices, scan temporaries): grow-only.
-  void* d_parse = nullptr;
-  size_t d_parse_cap = 0;
-  // Sorted varlen mode: run-sorted frame records (16 B per frame, sort_runs), grow-only.
-  void* d_rec = nullptr;
-  size_t d_rec_cap = 0;
+  // Kernel-selection options (ufc_ctx_set_option; A/B measurement and tests).
+  int opt[UFC_OPT_COUNT_] = {};
+  // Device scratch of the batch parse and of the sorted varlen mode, one grow-only buffer per
+  // (kind, stream): work queued on different streams never shares scratch.
+  struct Scratch {
+    int kind;
+    hipStream_t stream;
+    void* p;
+    size_t cap;
+  };
+  std::mutex scratch_mu;
+  std::vector<Scratch> scratch;
 };
 
 constexpr uint32_t kCtrSlots = 64;
 
 namespace {
+
+enum ScratchKind { kScratchParse = 0, kScratchSortRec = 1 };
+
+// The (kind, stream) scratch buffer of at least `need` bytes.  Growing waits for the work already
+// queued on that stream (the only user of the old buffer) before freeing it.
+hipError_t stream_scratch(ufc_ctx* ctx, int kind, hipStream_t stream, size_t need, void** out) {
+  std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+  ufc_ctx::Scratch* sc = nullptr;
+  for (auto& x : ctx->scratch)
+    if (x.kind == kind && x.stream == stream) sc = &x;
+  if (!sc) {
+    ctx->scratch.push_back({kind, stream, nullptr, 0});
+    sc = &ctx->scratch.back();
+  }
+  if (sc->cap < need) {
+    hipError_t e;
+    if (sc->p) {
+      if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+      (void)hipFree(sc->p);
+      sc->p = nullptr;
+      sc->cap = 0;
+    }
+    if ((e = hipMalloc(&sc->p, need)) != hipSuccess) return e;
+    sc->cap = need;
+  }
+  *out = sc->p;
+  return hipSuccess;
+}
 
 struct DeviceGuard {  // restores the caller's current device
   int prev = -1;
@@ -75,16 +110,6 @@ struct Config {
   int jc;  // 256-byte blocks per pipelined part
 };
 
-// Optional tuning override, e.g. UFC_FIXED_JC=3.
-bool env_config(const char* name, Config* c) {
-  const char* v = std::getenv(name);
-  if (!v) return false;
-  const int jc = std::atoi(v);
-  if (!ufc_dev::config_available(jc)) return false;
-  c->jc = jc;
-  return true;
-}
-
 int launch(ufc_ctx* ctx, Config cfg, int mode, ufc_dev::KernelParams& kp, hipStream_t stream) {
   const void* fn = ufc_dev::kernel_symbol(cfg.jc, mode);
   if (!fn) return UFC_ERR_INVALID_ARG;
@@ -105,31 +130,30 @@ int launch(ufc_ctx* ctx, Config cfg, int mode, ufc_dev::KernelParams& kp, hipStr
 }
 
 // Lean fixed-length kernel: J = blocks per frame when 4 <= frame_len and J <= 6, else 0.  The
-// generic kernel stays reachable with UFC_FIXED_KERNEL=generic (A/B measurement) or UFC_FIXED_JC.
-// The batch must also hold a full 4-frame set past the edge sets (those whose first frames' pad
-// bytes precede the buffer), which the kernel's out-of-range prefetches re-read.
-int lean_fixed_blocks(uint64_t frame_len, uint64_t stride, uint64_t n) {
+// generic kernel stays reachable with UFC_OPT_FIXED_KERNEL = UFC_FIXED_GENERIC or a
+// UFC_OPT_GENERIC_JC override (A/B measurement).  The batch must also hold a full 4-frame set
+// past the edge sets (those whose first frames' pad bytes precede the buffer), which the kernel's
+// out-of-range prefetches re-read.
+int lean_fixed_blocks(const ufc_ctx* ctx, uint64_t frame_len, uint64_t stride, uint64_t n) {
   if (frame_len < 4) return 0;
   const uint64_t J = (frame_len + 4 + 255) / 256;
   if (J > 6 || stride >= (1ull << 28)) return 0;  // lane offsets (3 strides + 2 KiB) stay below 2^31
   const uint64_t pad = 256 * J - frame_len;
   const uint64_t s_edge = (pad + 4 * stride - 1) / (4 * stride);
   if (n / 4 <= s_edge) return 0;
-  const char* k = std::getenv("UFC_FIXED_KERNEL");
-  if (k && std::strcmp(k, "generic") == 0) return 0;
-  if (std::getenv("UFC_FIXED_JC")) return 0;
+  if (ctx->opt[UFC_OPT_FIXED_KERNEL] == UFC_FIXED_GENERIC || ctx->opt[UFC_OPT_GENERIC_JC] != 0) return 0;
   return (int)J;
 }
 
-int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
+// front_ok: the bytes before the batch's first frame are readable (a later part of a larger batch).
+int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream,
+                      bool front_ok = false) {
   int depth = ufc_dev::kLeanDepthDefault, abl = 0, waves = ufc_dev::kLeanWavesDefault;
   int sched = ufc_dev::kLeanSchedDefault;
-  if (const char* cfg = std::getenv("UFC_LEAN_CFG")) {  // A/B: the previous default
-    if (std::strcmp(cfg, "claim16") == 0) {
-      depth = 3;
-      sched = ufc_dev::kSchedClaim;
-      waves = 16;
-    }
+  if (ctx->opt[UFC_OPT_FIXED_KERNEL] == UFC_FIXED_CLAIM16) {  // A/B: the round-1 default
+    depth = 3;
+    sched = ufc_dev::kSchedClaim;
+    waves = 16;
   }
 #ifdef UFC_TUNING
   // A/B knobs of the validate path (tuning builds): pipeline depth, schedule, ablations.
@@ -164,7 +188,7 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
     if (kp.wbytes) c.wbytes = kp.wbytes + f0 * kp.stride;
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
-    c.front_ok = f0 > 0 ? 1u : 0u;
+    c.front_ok = (f0 > 0 || front_ok) ? 1u : 0u;
 #ifdef UFC_TUNING
     if (std::getenv("UFC_FRONT_OK")) c.front_ok = 1u;  // A/B only: the caller guarantees readable pad bytes
 #endif
@@ -200,27 +224,21 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
   return UFC_OK;
 }
 
-// Lean variable-length kernel unless UFC_VARLEN_KERNEL=generic (A/B measurement).
-bool lean_varlen() {
-  const char* k = std::getenv("UFC_VARLEN_KERNEL");
-  return !(k && std::strcmp(k, "generic") == 0);
-}
+// Lean variable-length kernel unless UFC_OPT_VARLEN_KERNEL = UFC_VARLEN_GENERIC (A/B measurement).
+bool lean_varlen(const ufc_ctx* ctx) { return ctx->opt[UFC_OPT_VARLEN_KERNEL] != UFC_VARLEN_GENERIC; }
 
 int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream, bool pairs = false) {
   // Claimed sets, 16 waves: measured fastest for mixed lengths (compute-heavy per set; DESIGN.md
-  // section 5.2).  UFC_VL_CFG=blocked8: the static blocked schedule at 8 waves (A/B).
+  // section 5.2).  UFC_VARLEN_BLOCKED8: the static blocked schedule at 8 waves (A/B).
   int abl = 0, sched = ufc_dev::kSchedClaim, waves = 16;
-  if (const char* cfg = std::getenv("UFC_VL_CFG")) {
-    if (std::strcmp(cfg, "blocked8") == 0) {
-      sched = ufc_dev::kSchedBlocked;
-      waves = 8;
-    }
+  if (ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_BLOCKED8) {
+    sched = ufc_dev::kSchedBlocked;
+    waves = 8;
   }
-  // UFC_VL_SORT=1: frames sorted by block count within runs of 64 (ufc_dev::sort_runs) first.
+  // UFC_VARLEN_SORTED: frames sorted by block count within runs of 64 (ufc_dev::sort_runs) first.
   // Measured (config 3): compute -9 %, but the loads lose the neighbouring frames' shared lines
   // (loads only 1.67 -> 2.00 ms), 2.00 vs 1.88 ms overall, so it is off by default.
-  bool sorted = false;
-  if (const char* so = std::getenv("UFC_VL_SORT")) sorted = std::atoi(so) != 0;
+  bool sorted = ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_SORTED;
 #ifdef UFC_TUNING
   if (const char* ab = std::getenv("UFC_VL_ABL")) abl = std::atoi(ab);
   if (const char* sc = std::getenv("UFC_VL_SCHED")) sched = std::atoi(sc);
@@ -239,26 +257,20 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
   const uint64_t chunk = sorted ? (uint64_t)1 << 29 : (uint64_t)1 << 31;
   const uint64_t total = kp.nframes;
   hipError_t e;
+  void* rec = nullptr;
   if (sorted) {
     const size_t need = (size_t)((std::min(chunk, total) + 63) / 64 * 64) * 16;
-    if (ctx->d_rec_cap < need) {  // grows on the first (or a larger) batch only
-      if (ctx->d_rec && (e = hipStreamSynchronize(stream)) != hipSuccess) return hip_fail(ctx, e);
-      if (ctx->d_rec) (void)hipFree(ctx->d_rec);
-      ctx->d_rec = nullptr;
-      ctx->d_rec_cap = 0;
-      if ((e = hipMalloc(&ctx->d_rec, need)) != hipSuccess) return hip_fail(ctx, e);
-      ctx->d_rec_cap = need;
-    }
+    if ((e = stream_scratch(ctx, kScratchSortRec, stream, need, &rec)) != hipSuccess) return hip_fail(ctx, e);
   }
   for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
     c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
     if (sorted) {
-      if ((e = (hipError_t)ufc_dev::sort_runs(c.offsets, pairs, c.nframes, ctx->d_rec, stream)) != hipSuccess)
+      if ((e = (hipError_t)ufc_dev::sort_runs(c.offsets, pairs, c.nframes, rec, stream)) != hipSuccess)
         return hip_fail(ctx, e);
       c.offsets_csr = pairs ? nullptr : c.offsets;
-      c.offsets = (const uint64_t*)ctx->d_rec;
+      c.offsets = (const uint64_t*)rec;
     }
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
@@ -276,20 +288,20 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
 }
 
 // Kernel configuration and mode bits for a fixed frame length: J = 256-byte blocks per frame.
-Config fixed_config(uint64_t frame_len, int* freeze) {
+Config fixed_config(const ufc_ctx* ctx, uint64_t frame_len, int* freeze) {
   const uint64_t n = frame_len >= 4 ? frame_len - 4 : frame_len;
   const uint64_t J = (n + 8 + 255) / 256;  // virtual stream: G + n bytes + trailer, 256-B blocks
   Config c;
-  if (!env_config("UFC_FIXED_JC", &c)) c.jc = J <= 6 ? (int)J : 6;
+  const int jc = ctx->opt[UFC_OPT_GENERIC_JC];
+  c.jc = ufc_dev::config_available(jc) ? jc : (J <= 6 ? (int)J : 6);
   // Without freeze the kernel assumes one part per set (JC == J); anything else runs in freeze mode.
   *freeze = ((uint64_t)c.jc == J) ? 0 : ufc_dev::kModeFreeze;
   return c;
 }
 
-Config varlen_config() {
-  Config c = {3};
-  env_config("UFC_VARLEN_JC", &c);
-  return c;
+Config varlen_config(const ufc_ctx* ctx) {
+  const int jc = ctx->opt[UFC_OPT_GENERIC_JC];
+  return Config{ufc_dev::config_available(jc) ? jc : 3};
 }
 
 constexpr uint64_t kMaxFrameLen = (uint64_t)1 << 30;  // per-frame limit of the 32-bit offsets math
@@ -340,11 +352,35 @@ const char* ufc_error_string(int code) {
     case UFC_ERR_NO_DEVICE: return "no usable gfx950 (MI355X) device";
     case UFC_ERR_HIP: return "HIP runtime error (see ufc_ctx_last_hip_error)";
     case UFC_ERR_NOMEM: return "out of memory";
+    case UFC_ERR_COMM: return "RCCL unavailable or failed (see ufc_comm_last_error)";
     default: return "unknown error";
   }
 }
 
 int ufc_ctx_last_hip_error(const ufc_ctx* ctx) { return ctx ? ctx->last_hip_error : 0; }
+
+int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
+  if (!ctx || option < 0 || option >= UFC_OPT_COUNT_) return UFC_ERR_INVALID_ARG;
+  switch (option) {
+    case UFC_OPT_FIXED_KERNEL:
+      if (value < UFC_FIXED_AUTO || value > UFC_FIXED_CLAIM16) return UFC_ERR_INVALID_ARG;
+      break;
+    case UFC_OPT_VARLEN_KERNEL:
+      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_BLOCKED8) return UFC_ERR_INVALID_ARG;
+      break;
+    case UFC_OPT_GENERIC_JC:
+      if (value != 0 && !ufc_dev::config_available(value)) return UFC_ERR_INVALID_ARG;
+      break;
+    default: return UFC_ERR_INVALID_ARG;
+  }
+  ctx->opt[option] = value;
+  return UFC_OK;
+}
+
+int ufc_ctx_get_option(const ufc_ctx* ctx, int option) {
+  if (!ctx || option < 0 || option >= UFC_OPT_COUNT_) return UFC_ERR_INVALID_ARG;
+  return ctx->opt[option];
+}
 
 int ufc_ctx_create(ufc_ctx** out, int device) {
   if (!out) return UFC_ERR_INVALID_ARG;
@@ -376,6 +412,17 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
     return UFC_ERR_HIP;
   }
   // The kernels declare their 160 KiB of LDS statically: no dynamic-LDS attribute to set.
+#ifdef UFC_TUNING
+  // Tuning builds: the A/B scripts select kernels through the environment (read once, here).
+  if (const char* k = std::getenv("UFC_FIXED_KERNEL"))
+    ctx->opt[UFC_OPT_FIXED_KERNEL] = std::strcmp(k, "generic") == 0 ? UFC_FIXED_GENERIC
+                                     : std::strcmp(k, "claim16") == 0 ? UFC_FIXED_CLAIM16 : UFC_FIXED_AUTO;
+  if (const char* k = std::getenv("UFC_VARLEN_KERNEL"))
+    ctx->opt[UFC_OPT_VARLEN_KERNEL] = std::strcmp(k, "generic") == 0 ? UFC_VARLEN_GENERIC
+                                      : std::strcmp(k, "sorted") == 0 ? UFC_VARLEN_SORTED
+                                      : std::strcmp(k, "blocked8") == 0 ? UFC_VARLEN_BLOCKED8 : UFC_VARLEN_AUTO;
+  if (const char* j = std::getenv("UFC_FIXED_JC")) ctx->opt[UFC_OPT_GENERIC_JC] = std::atoi(j);
+#endif
   *out = ctx;
   return UFC_OK;
 }
@@ -387,8 +434,8 @@ int ufc_ctx_destroy(ufc_ctx* ctx) {
     if (ctx->d_chain) (void)hipFree(ctx->d_chain);
     if (ctx->d_nib) (void)hipFree(ctx->d_nib);
     if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
-    if (ctx->d_parse) (void)hipFree(ctx->d_parse);
-    if (ctx->d_rec) (void)hipFree(ctx->d_rec);
+    for (auto& sc : ctx->scratch)
+      if (sc.p) (void)hipFree(sc.p);
     if (ctx->d_stage) (void)hipFree(ctx->d_stage);
     if (ctx->d_off) (void)hipFree(ctx->d_off);
     if (ctx->d_crc) (void)hipFree(ctx->d_crc);
@@ -403,13 +450,27 @@ int ufc_ctx_destroy(ufc_ctx* ctx) {
 
 int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
                         uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream) {
+  return ufc_internal::crc_fixed(ctx, d_frames, stride, frame_len, n, d_crc_out, d_valid_out, (hipStream_t)stream,
+                                 false);
+}
+
+}  // extern "C"
+
+int ufc_internal::ctx_device(const ufc_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+void ufc_internal::note_hip_error(ufc_ctx* ctx, int e) {
+  if (ctx) ctx->last_hip_error = e;
+}
+
+int ufc_internal::crc_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
+                            uint32_t* d_crc_out, uint8_t* d_valid_out, hipStream_t stream, bool front_ok) {
   if (!ctx) return UFC_ERR_INVALID_ARG;
   if (n == 0) return UFC_OK;
   if (!d_frames || stride < frame_len || frame_len > kMaxFrameLen || (!d_crc_out && !d_valid_out))
     return UFC_ERR_INVALID_ARG;
   int freeze;
-  const Config cfg = fixed_config(frame_len, &freeze);
-  int lean = lean_fixed_blocks(frame_len, stride, n);
+  const Config cfg = fixed_config(ctx, frame_len, &freeze);
+  int lean = lean_fixed_blocks(ctx, frame_len, stride, n);
 #ifdef UFC_TUNING
   if (const char* ab = std::getenv("UFC_ABLATE")) {
     freeze |= std::atoi(ab);
@@ -424,9 +485,11 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
-  if (lean) return launch_lean_fixed(ctx, lean, false, kp, (hipStream_t)stream);
-  return launch(ctx, cfg, freeze, kp, (hipStream_t)stream);
+  if (lean) return launch_lean_fixed(ctx, lean, false, kp, stream, front_ok);
+  return launch(ctx, cfg, freeze, kp, stream);
 }
+
+extern "C" {
 
 int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
                          uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream) {
@@ -440,8 +503,8 @@ int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
-  if (lean_varlen()) return launch_lean_varlen(ctx, false, kp, (hipStream_t)stream);
-  return launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, (hipStream_t)stream);
+  if (lean_varlen(ctx)) return launch_lean_varlen(ctx, false, kp, (hipStream_t)stream);
+  return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen, kp, (hipStream_t)stream);
 }
 
 int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
@@ -450,7 +513,7 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   if (n == 0) return UFC_OK;
   if (!d_frames || stride < frame_len || frame_len < 4 || frame_len > kMaxFrameLen) return UFC_ERR_INVALID_ARG;
   int freeze;
-  const Config cfg = fixed_config(frame_len, &freeze);
+  const Config cfg = fixed_config(ctx, frame_len, &freeze);
   ufc_dev::KernelParams kp{};
   kp.bytes = d_frames;
   kp.wbytes = d_frames;
@@ -459,7 +522,7 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
-  if (const int lean = lean_fixed_blocks(frame_len, stride, n))
+  if (const int lean = lean_fixed_blocks(ctx, frame_len, stride, n))
     return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
   return launch(ctx, cfg, freeze | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
@@ -476,12 +539,12 @@ int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offs
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
-  if (lean_varlen()) return launch_lean_varlen(ctx, true, kp, (hipStream_t)stream);
-  return launch(ctx, varlen_config(), ufc_dev::kModeVarlen | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
+  if (lean_varlen(ctx)) return launch_lean_varlen(ctx, true, kp, (hipStream_t)stream);
+  return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
 
-int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
-                             uint32_t* h_crc_out, uint8_t* h_valid_out) {
+static int validate_host_varlen_impl(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
+                                     uint32_t* h_crc_out, uint8_t* h_valid_out) {
   if (!ctx) return UFC_ERR_INVALID_ARG;
   if (n == 0) return UFC_OK;
   if (!h_bytes || !h_offsets || (!h_crc_out && !h_valid_out)) return UFC_ERR_INVALID_ARG;
@@ -562,7 +625,7 @@ int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_
     kp.nframes = nf;
     kp.crc_out = dcrc;
     kp.valid_out = dval;
-    int rc = lean_varlen() ? launch_lean_varlen(ctx, false, kp, s) : launch(ctx, varlen_config(), ufc_dev::kModeVarlen, kp, s);
+    int rc = lean_varlen(ctx) ? launch_lean_varlen(ctx, false, kp, s) : launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen, kp, s);
     if (rc != UFC_OK) return rc;
     if (h_crc_out && (e = hipMemcpyAsync(h_crc_out + a, dcrc, nf * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
       return hip_fail(ctx, e);
@@ -590,8 +653,8 @@ int ufc_crc_batch_pairs(ufc_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, 
   return launch_lean_varlen(ctx, false, kp, (hipStream_t)stream, true);
 }
 
-int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
-                            size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out) {
+static int validate_host_slots_impl(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
+                                    size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out) {
   if (!ctx) return UFC_ERR_INVALID_ARG;
   if (n == 0) return UFC_OK;
   if (!h_slots || !h_lens || slot_stride == 0 || (!h_crc_out && !h_valid_out)) return UFC_ERR_INVALID_ARG;
@@ -664,6 +727,28 @@ int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_st
   return UFC_OK;
 }
 
+// After a failure part-way through a host-buffer call, copies of earlier chunks may still be
+// queued on the context's streams (reading the caller's frames, writing its outputs): wait for
+// them before returning, so that nothing touches the caller's buffers after the call.
+static int drain_on_error(ufc_ctx* ctx, int rc) {
+  if (rc != UFC_OK && ctx)
+    for (hipStream_t s : ctx->streams)
+      if (s) (void)hipStreamSynchronize(s);
+  return rc;
+}
+
+int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
+                             uint32_t* h_crc_out, uint8_t* h_valid_out) {
+  DeviceGuard g(ctx ? ctx->device : 0);
+  return drain_on_error(ctx, validate_host_varlen_impl(ctx, h_bytes, h_offsets, n, h_crc_out, h_valid_out));
+}
+
+int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
+                            size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out) {
+  DeviceGuard g(ctx ? ctx->device : 0);
+  return drain_on_error(ctx, validate_host_slots_impl(ctx, h_slots, slot_stride, h_lens, n, h_crc_out, h_valid_out));
+}
+
 namespace {
 void put_trailer(uint8_t* f, size_t len, uint32_t crc) {  // serial/mod.rs:466-470
   uint8_t* t = f + len - 4;
@@ -677,6 +762,8 @@ void put_trailer(uint8_t* f, size_t len, uint32_t crc) {  // serial/mod.rs:466-4
 int ufc_seal_host_slots(ufc_ctx* ctx, uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens, size_t n,
                         uint32_t* h_crc_scratch) {
   if (!ctx || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!h_slots || !h_lens) return UFC_ERR_INVALID_ARG;
   for (size_t i = 0; i < n; i++)
     if (h_lens[i] < 4) return UFC_ERR_INVALID_ARG;
   // The gate computes crc = compute(frame[..len-4]) whatever the trailer holds: that is the seal.
@@ -689,6 +776,8 @@ int ufc_seal_host_slots(ufc_ctx* ctx, uint8_t* h_slots, size_t slot_stride, cons
 int ufc_seal_host_varlen(ufc_ctx* ctx, uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
                          uint32_t* h_crc_scratch) {
   if (!ctx || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!h_bytes || !h_offsets) return UFC_ERR_INVALID_ARG;
   for (size_t i = 0; i < n; i++)
     if (h_offsets[i + 1] < h_offsets[i] + 4) return UFC_ERR_INVALID_ARG;
   const int rc = ufc_validate_host_varlen(ctx, h_bytes, h_offsets, n, h_crc_scratch, nullptr);
@@ -706,18 +795,12 @@ int ufc_parse_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t*
   DeviceGuard g(ctx->device);
   hipError_t e;
   const size_t need = ufc_dev::parse_scratch_bytes(n);
-  if (ctx->d_parse_cap < need) {  // grows on the first (or a larger) batch only
-    if (ctx->d_parse && (e = hipStreamSynchronize((hipStream_t)stream)) != hipSuccess) return hip_fail(ctx, e);
-    if (ctx->d_parse) (void)hipFree(ctx->d_parse);
-    ctx->d_parse = nullptr;
-    ctx->d_parse_cap = 0;
-    if ((e = hipMalloc(&ctx->d_parse, need)) != hipSuccess) return hip_fail(ctx, e);
-    ctx->d_parse_cap = need;
-  }
+  void* scratch = nullptr;  // this stream's own scratch (grows on the first or a larger batch only)
+  if ((e = stream_scratch(ctx, kScratchParse, (hipStream_t)stream, need, &scratch)) != hipSuccess)
+    return hip_fail(ctx, e);
   ufc_dev::ParseArgs a{d_bytes, d_offsets, (uint64_t)n, d_valid, d_infos, d_items, (uint64_t)(d_items ? items_cap : 0),
                        d_items_used};
-  if ((e = ufc_dev::parse_batch(a, ctx->d_parse, ctx->d_parse_cap, (hipStream_t)stream)) != hipSuccess)
-    return hip_fail(ctx, e);
+  if ((e = ufc_dev::parse_batch(a, scratch, need, (hipStream_t)stream)) != hipSuccess) return hip_fail(ctx, e);
   return UFC_OK;
 }
 

@@ -32,7 +32,7 @@ FRAME_INFO_DTYPE = np.dtype([("kind", "u1"), ("ok", "u1"), ("aux", "u1"), ("crc_
                              ("item_count", "<u4"), ("item_first", "<u4")])
 ITEM_DTYPE = np.dtype([("id", "<u4"), ("channel_id", "u1"), ("form", "u1"), ("window_parent_lead", "<u2"),
                        ("channel_parent_lead", "<u2"), ("fragment_id", "<u2"), ("fragment_id_last", "<u2"),
-                       ("reserved", "<u2"), ("data_offset", "<u4"), ("data_len", "<u4")])
+                       ("flags", "<u2"), ("data_offset", "<u4"), ("data_len", "<u4")])
 assert FRAME_INFO_DTYPE.itemsize == ctypes.sizeof(FrameInfo) == 32
 assert ITEM_DTYPE.itemsize == ctypes.sizeof(Item) == 24
 
@@ -112,6 +112,24 @@ class AckFrame:
     frame_window_base_id: int
     packet_window_base_id: int
     frame_acks: List[AckGroup] = field(default_factory=list)
+
+
+MAX_FRAGMENT_SIZE = 1448  # src/lib.rs:297
+
+
+def datagram_is_valid(dg: Datagram) -> bool:
+    """src/half_connection/packet_receiver/mod.rs:12-30 (through ufc_datagram_is_valid)."""
+    it = Item()
+    it.channel_id = dg.channel_id & 0xFF
+    it.window_parent_lead = dg.window_parent_lead & 0xFFFF
+    it.channel_parent_lead = dg.channel_parent_lead & 0xFFFF
+    it.fragment_id = dg.fragment_id & 0xFFFF
+    it.fragment_id_last = dg.fragment_id_last & 0xFFFF
+    it.data_len = len(dg.data)
+    rc = lib().ufc_datagram_is_valid(ctypes.byref(it))
+    if rc < 0:
+        check(rc, "ufc_datagram_is_valid")
+    return rc == 1
 
 
 def _u8buf(data):

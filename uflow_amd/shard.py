@@ -1,86 +1,88 @@
-"""Multi-GPU path: frames shard by frame index across ranks (one process per GPU); the only
-exchange is gathering the per-frame CRC words (and valid flags) to the root over RCCL/xGMI.
+"""Multi-GPU path: a batch of frames shards by frame index across ranks (one process per GPU); the
+only exchange is gathering the per-frame CRC words and valid flags to a root over RCCL/xGMI
+(SURVEY.md section 8(e)).  Both halves live in libuflowcrc.so's C ABI (ufc_crc_sharded,
+include/uflow_frame_crc.h), so a Rust host reaches the same path as this binding.
 
-There is no data-path collective: every rank validates its own contiguous frame range, which is
-the natural partition of independent frames.
+There is no data-path collective: every rank validates its own contiguous frame range.
 """
+import ctypes
+
 import torch
-import torch.distributed as dist
+
+from ._native import UFC_COMM_ID_BYTES, check, lib
 
 
 def shard_range(total, rank, world):
-    """Contiguous frame range [lo, hi) of `rank` (sizes differ by at most one)."""
+    """Contiguous frame range [lo, hi) of `rank` (sizes differ by at most one): ufc_shard_range."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError("bad rank/world")
-    lo = total * rank // world
-    hi = total * (rank + 1) // world
-    return lo, hi
+    first, count = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().ufc_shard_range(total, world, rank, ctypes.byref(first), ctypes.byref(count)), "ufc_shard_range")
+    return first.value, first.value + count.value
 
 
-def gather_to_root(local, total, root=0, group=None):
-    """Gather each rank's shard (1-D tensor, rank r holds shard_range(total, r, world)) into one
-    tensor of length `total` on `root` (None elsewhere).  Uses dist.gather, which is RCCL's
-    point-to-point gather on the nccl backend; shards are padded to equal length."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    maxlen = (total + world - 1) // world
-    buf = torch.zeros(maxlen, dtype=local.dtype, device=local.device)
-    buf[: local.numel()] = local
-    parts = [torch.empty_like(buf) for _ in range(world)] if rank == root else None
-    dist.gather(buf, gather_list=parts, dst=root, group=group)
-    if rank != root:
-        return None
-    out = torch.empty(total, dtype=local.dtype, device=local.device)
-    for r in range(world):
-        lo, hi = shard_range(total, r, world)
-        out[lo:hi] = parts[r][: hi - lo]
+def shard_chunks(total, rank, world):
+    """The gather pipeline's chunks of `rank`'s shard as global [lo, hi) ranges (ufc_shard_chunk):
+    chunk c of every rank is gated, then sent, in the same order on every rank."""
+    first, count = ctypes.c_uint64(), ctypes.c_uint64()
+    k = lib().ufc_shard_chunk(total, world, rank, 0, ctypes.byref(first), ctypes.byref(count))
+    if k < 0:
+        check(k, "ufc_shard_chunk")
+    out = []
+    for c in range(k):
+        rc = lib().ufc_shard_chunk(total, world, rank, c, ctypes.byref(first), ctypes.byref(count))
+        if rc < 0:
+            check(rc, "ufc_shard_chunk")
+        out.append((first.value, first.value + count.value))
     return out
 
 
-class ShardGatherer:
-    """Preallocated, pipelined gather of per-frame results to the root (bench.py's multi-GPU step).
+def comm_id_create():
+    """A fresh communicator id (ncclGetUniqueId), made on one rank and handed to the others."""
+    buf = (ctypes.c_uint8 * UFC_COMM_ID_BYTES)()
+    check(lib().ufc_comm_id_create(buf), "ufc_comm_id_create")
+    return bytes(buf)
 
-    Every rank holds `n_local` frames.  Slot i owns one byte buffer: the CRC words (4 B per frame)
-    followed by the valid flags (1 B per frame), so the kernel writes straight into it and ONE
-    gather (RCCL point-to-point on the nccl backend) moves both.  Slots rotate: the gather of step
-    k (async, on the collective's stream) overlaps the kernel of step k+1, which writes the other
-    slot; `wait(i)` makes the current stream wait for slot i's previous gather before it is
-    rewritten.  Nothing is allocated per step.
-    """
 
-    def __init__(self, n_local, device, root=0, depth=2, group=None):
-        self.n = n_local
-        self.root = root
-        self.group = group
-        self.world = dist.get_world_size(group)
-        self.rank = dist.get_rank(group)
-        self.bufs = [torch.zeros(5 * n_local, dtype=torch.uint8, device=device) for _ in range(depth)]
-        self.recv = [torch.zeros((self.world, 5 * n_local), dtype=torch.uint8, device=device)
-                     if self.rank == root else None for _ in range(depth)]
-        self.handles = [None] * depth
+class ShardedGate:
+    """ufc_comm over one FrameCrcEngine (this rank's GPU): the batched gate over this rank's shard
+    of a global fixed-length batch and the RCCL gather of CRC words + valid flags to the root."""
 
-    def outputs(self, i):
-        """(crc int32[n], valid uint8[n]) views of slot i, for the kernel to write."""
-        b = self.bufs[i]
-        return b[: 4 * self.n].view(torch.int32), b[4 * self.n:]
+    def __init__(self, engine, world, rank, comm_id: bytes):
+        if len(comm_id) != UFC_COMM_ID_BYTES:
+            raise ValueError("comm id must be %d bytes" % UFC_COMM_ID_BYTES)
+        self.engine, self.world, self.rank = engine, world, rank
+        self._comm = ctypes.c_void_p()
+        idbuf = (ctypes.c_uint8 * UFC_COMM_ID_BYTES).from_buffer_copy(comm_id)
+        check(lib().ufc_comm_create(ctypes.byref(self._comm), engine._ctx, world, rank, idbuf), "ufc_comm_create")
 
-    def start(self, i):
-        parts = list(self.recv[i].unbind(0)) if self.rank == self.root else None
-        self.handles[i] = dist.gather(self.bufs[i], gather_list=parts, dst=self.root, group=self.group,
-                                      async_op=True)
+    def close(self):
+        if self._comm:
+            lib().ufc_comm_destroy(self._comm)
+            self._comm = ctypes.c_void_p()
 
-    def wait(self, i):
-        if self.handles[i] is not None:
-            self.handles[i].wait()
-            self.handles[i] = None
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
-    def wait_all(self):
-        for i in range(len(self.handles)):
-            self.wait(i)
+    def local_range(self, n_total):
+        return shard_range(n_total, self.rank, self.world)
 
-    def gathered(self, i):
-        """On the root, after wait(i): (crc int32[world*n], valid uint8[world*n]) in global frame order."""
-        if self.rank != self.root:
-            return None
-        r = self.recv[i]
-        return r[:, : 4 * self.n].contiguous().view(torch.int32).reshape(-1), r[:, 4 * self.n:].reshape(-1)
+    def crc_sharded(self, frames, frame_len, n_total, crc_out, valid_out, root=0, stride=None, stream=None,
+                    gather_stream=None):
+        """frames: this rank's shard (uint8, frame k at k * stride).  crc_out / valid_out: on the root
+        n_total entries in global frame order, elsewhere this rank's shard.  The gate runs on
+        `stream` (default: current), the transfers on `gather_stream` (default: `stream`)."""
+        stride = frame_len if stride is None else stride
+        lo, hi = self.local_range(n_total)
+        n_out = n_total if self.rank == root else hi - lo
+        eng = self.engine
+        eng._check("frames", frames, (torch.uint8,), (hi - lo - 1) * stride + frame_len if hi > lo else 0)
+        eng._check_outputs(n_out, crc_out, valid_out)
+        s = eng._stream(stream)
+        gs = eng._stream(gather_stream) if gather_stream is not None else None
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        check(lib().ufc_crc_sharded(self._comm, p(frames), stride, frame_len, n_total, p(crc_out), p(valid_out), root,
+                                    s, gs), "ufc_crc_sharded")
