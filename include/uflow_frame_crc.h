@@ -86,10 +86,12 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 #define UFC_FIXED_GENERIC 1      /*   the generic kernel */
 #define UFC_FIXED_CLAIM16 2      /*   lean kernel, claimed schedule at 16 waves (round-1 default) */
 #define UFC_OPT_VARLEN_KERNEL 1  /* CSR / pairs batches: */
-#define UFC_VARLEN_AUTO 0        /*   default */
+#define UFC_VARLEN_AUTO 0        /*   the default (currently UFC_VARLEN_SORTED) */
 #define UFC_VARLEN_GENERIC 1     /*   the generic kernel */
-#define UFC_VARLEN_SORTED 2      /*   frames sorted by block count within runs of 64 first */
-#define UFC_VARLEN_BLOCKED8 3    /*   static blocked schedule at 8 waves */
+#define UFC_VARLEN_SORTED 2      /*   round-1 kernel on frames sorted by block count within runs of 64 */
+#define UFC_VARLEN_BLOCKED8 3    /*   round-1 kernel, static blocked schedule at 8 waves */
+#define UFC_VARLEN_CLAIM16 4     /*   round-1 kernel, claimed sets at 16 waves (round-1 default) */
+#define UFC_VARLEN_BLOCKSTREAM 5 /*   sorted block-stream kernel (one 1-KB block step at a time) */
 #define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
 #define UFC_OPT_COUNT_ 3
 int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value);

@@ -392,12 +392,14 @@ def test_fixed_multi_launch(engine, frame_len, extra):
         assert np.array_equal(got, ref_crc)
 
 
-@pytest.mark.parametrize("mode", ["sorted", "blocked8", "generic"])
+@pytest.mark.parametrize("mode", ["sorted", "blocked8", "generic", "claim16", "blockstream"])
 def test_varlen_alternate_modes(engine, mode):
-    """The varlen kernel's A/B modes (ufc_ctx_set_option): run-sorted records, the static blocked
-    schedule at 8 waves, the generic kernel -- mixed lengths, edge lengths, seal, gapped pairs."""
+    """The varlen kernel's A/B modes (ufc_ctx_set_option): run-sorted records (the default, set
+    explicitly), the static blocked schedule at 8 waves, the generic kernel, the claimed unsorted
+    sets, the block-stream kernel -- mixed lengths, edge lengths, seal, gapped pairs."""
     from uflow_amd import _native as N
-    value = {"sorted": N.UFC_VARLEN_SORTED, "blocked8": N.UFC_VARLEN_BLOCKED8, "generic": N.UFC_VARLEN_GENERIC}[mode]
+    value = {"sorted": N.UFC_VARLEN_SORTED, "blocked8": N.UFC_VARLEN_BLOCKED8, "generic": N.UFC_VARLEN_GENERIC,
+             "claim16": N.UFC_VARLEN_CLAIM16, "blockstream": N.UFC_VARLEN_BLOCKSTREAM}[mode]
     engine.set_option(N.UFC_OPT_VARLEN_KERNEL, value)
     try:
         assert engine.get_option(N.UFC_OPT_VARLEN_KERNEL) == value
@@ -442,9 +444,11 @@ def test_parse_two_streams(engine):
             with torch.cuda.stream(s):
                 outs.append(engine.parse_varlen(d, o, valid, stream=s))
     torch.cuda.synchronize()
-    for got in outs:
-        for a, b in zip(got, ref):
-            assert torch.equal(a.cpu(), b)
+    k = int(ref[2][0])  # items past items_used are not written
+    for infos, items, used in outs:
+        assert torch.equal(infos.cpu(), ref[0])
+        assert int(used.cpu()[0]) == k
+        assert torch.equal(items[:k].cpu(), ref[1][:k])
 
 
 def test_fixed_random_shapes(engine):

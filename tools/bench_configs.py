@@ -1,14 +1,18 @@
-"""Secondary measurements for DESIGN.md (BASELINE.json configs 3, 4-per-GPU and 5), one JSON line
-each.  Not the driver's bench (bench.py is); run on the GPU box:  python tools/bench_configs.py
+"""Secondary measurements for DESIGN.md (BASELINE.json configs 3, 4-per-GPU and 5, the seal and the
+parse), one JSON line each.  Not the driver's bench (bench.py is); run on the GPU box:
+    python tools/bench_configs.py [--only varlen,shard,seal,parse,host] [--reps 20]
 
-  varlen   config 3: 10M frames, lengths U[64,1500] (seed 0x5EED0002), CSR offsets, device-resident;
-           GiB/s on the sum of frame lengths, kernel time from HIP events.
-  shard    config 4, one GPU's shard: 12.5M x 1500-B frames (18.75 GB) device-resident (the
-           batch spans several launches of the lean kernel).
+  varlen   config 3: 10M frames, lengths U[64,1500] (splitmix64, seed 0x5EED0002), CSR offsets,
+           device-resident; every frame checked against the oracle; CPU baseline of the same loop
+           (1 thread and all threads) on a sample.
+  shard    config 4, one GPU's shard: frames [37.5M, 50M) of the 100M-frame batch (seed 0x5EED0003),
+           18.75 GB device-resident (3 launches of the lean kernel).
   seal     the encode side of config 2: 1M x 1500-B frames sealed in place on the device.
+  parse    Frame::read past the gate on the device (ufc_parse_batch_varlen): 1M real uflow frames.
   host     config 5's GPU leg: 1M x 1472-B frames (uflow's MAX_FRAME_SIZE) that start and end in
            host memory -> ufc_validate_host_varlen (H2D + CRC + D2H) from pinned and from pageable
            buffers; GiB/s of frame bytes including the copies.
+Kernel times are HIP-event medians over --reps launches on the current stream.
 """
 import argparse
 import json
@@ -22,59 +26,91 @@ sys.path.insert(0, REPO)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+import oracle  # noqa: E402  (the checker and the CPU baseline only)
+from uflow_amd import synth  # noqa: E402
 from uflow_amd.batch import FrameCrcEngine  # noqa: E402
 
+PEAK = 8e12
 
-def timed(fn, reps, stream):
+
+def timed(fn, reps):
+    s = torch.cuda.current_stream()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for e0, e1 in evs:
-        e0.record(stream)
+        e0.record(s)
         fn()
-        e1.record(stream)
+        e1.record(s)
     torch.cuda.synchronize()
-    return float(np.median([a.elapsed_time(b) for a, b in evs]))
+    t = [a.elapsed_time(b) for a, b in evs]
+    return float(np.median(t)), float(np.mean(t))
 
 
-def varlen(eng, dev, n=10_000_000, reps=20):
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED0002)
-    lens = torch.randint(64, 1501, (n,), generator=g, device=dev, dtype=torch.int64)
-    offsets = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    offsets[1:] = torch.cumsum(lens, 0)
-    total = int(offsets[-1])
-    data = torch.randint(0, 256, (total,), generator=g, device=dev, dtype=torch.uint8)
+def settle(fn, ms=50):
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < ms:
+        fn()
+        torch.cuda.synchronize()
+
+
+def threads():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def rates(name, nbytes, algo, med, mean, **kw):
+    return {"config": name, "kernel_ms": round(med, 4), "kernel_mean_ms": round(mean, 4),
+            "GiB_s": round(nbytes / med / 1e-3 / 2**30, 1), "algo_GB_s": round(algo / med / 1e-3 / 1e9, 1),
+            "hbm_frac": round(algo / med / 1e-3 / PEAK, 4), "algorithmic_bytes": algo, **kw}
+
+
+def varlen(eng, dev, reps, n=10_000_000):
+    data, offsets = synth.varlen_batch(n, 64, 1500, synth.SEED_CONFIG3, device=dev)
     eng.seal_varlen(data, offsets)
-    data[offsets[:-1:997] + 7] ^= 0x20  # flip one bit in every 997th frame
+    flipped = torch.arange(0, n, 997, device=dev)
+    synth.flip_bits(data, offsets[flipped], byte_in_frame=7, mask=0x20)
     crc = torch.empty(n, dtype=torch.int32, device=dev)
     valid = torch.empty(n, dtype=torch.uint8, device=dev)
-    s = torch.cuda.current_stream()
     fn = lambda: eng.crc_varlen(data, offsets, crc_out=crc, valid_out=valid)  # noqa: E731
     fn()
     torch.cuda.synchronize()
-    expect = n - len(range(0, n, 997))
-    ok = int(valid.sum()) == expect
-    # bit-exact check of a sample (the first 200k frames) against the CPU oracle
-    import oracle
-    k = 200_000
-    off_h = offsets[: k + 1].cpu().numpy().astype(np.uint64)
-    ref_crc, ref_valid = oracle.validate_varlen(data[: int(off_h[-1])].cpu().numpy(), off_h)
-    exact = bool(np.array_equal(crc[:k].cpu().numpy().view(np.uint32), ref_crc) and
-                 np.array_equal(valid[:k].cpu().numpy(), ref_valid))
-    ms = timed(fn, reps, s)
-    os.environ["UFC_VARLEN_KERNEL"] = "generic"  # A/B: the generic kernel on the same batch
-    ms_generic = timed(fn, reps, s)
-    del os.environ["UFC_VARLEN_KERNEL"]
+    total = int(offsets[-1])
+    h_data, h_off = data.cpu().numpy(), offsets.cpu().numpy().astype(np.uint64)
+    ref_crc, ref_valid = oracle.validate_varlen_mt(h_data, h_off, min(64, threads()))
+    exact = bool(np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc) and
+                 np.array_equal(valid.cpu().numpy(), ref_valid))
+    settle(fn)
+    med, mean = timed(fn, reps)
+    # A/B: the round-1 kernel (claimed 16-wave sets of 4 consecutive frames) on the same batch
+    from uflow_amd import _native as N
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_CLAIM16)
+    settle(fn)
+    med_r1, _ = timed(fn, reps)
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_AUTO)
+    # CPU baseline: the oracle's bytewise loop (crc.rs:94-100) on the first frames, 1 thread and all
+    k1, kn = 50_000, min(n, 50_000 * threads())
+
+    def cpu(k, t):
+        o = h_off[: k + 1]
+        t0 = time.perf_counter()
+        oracle.validate_varlen_mt(h_data, o, t)
+        return (int(o[-1]) - int(o[0])) / (time.perf_counter() - t0) / 2**30
+
+    cpu1, cpun = cpu(k1, 1), cpu(kn, threads())
     algo = total + 8 * (n + 1) + 4 * n + n
-    return {"config": "3: varlen 10M x U[64,1500] device-resident", "frames": n, "bytes": total,
-            "kernel_ms": round(ms, 4), "GiB_s": round(total / ms / 1e-3 / 2**30, 1),
-            "algo_GB_s": round(algo / ms / 1e-3 / 1e9, 1), "hbm_frac": round(algo / ms / 1e-3 / 8e12, 4),
-            "valid_ok": ok, "sample_bit_exact": exact, "generic_kernel_ms": round(ms_generic, 4)}
+    return rates("3: varlen 10M x U[64,1500] device-resident", total, algo, med, mean, frames=n, bytes=total,
+                 bit_exact_all_frames=exact, valid_count_ok=int(ref_valid.sum()) == n - flipped.numel(),
+                 round1_kernel_ms=round(med_r1, 4),
+                 cpu_baseline={"unit": "GiB/s", "single_thread": round(cpu1, 4), "all_threads": round(cpun, 3),
+                               "threads": threads(), "nproc": os.cpu_count(),
+                               "sample": f"first {k1} frames on 1 thread, first {kn} frames on {threads()} threads"})
 
 
-def shard(eng, dev, n=12_500_000, L=1500, reps=10):
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED0003)
-    frames = torch.randint(0, 256, (n * L,), generator=g, device=dev, dtype=torch.uint8)
+def shard(eng, dev, reps, world=8, rank=3, total=100_000_000, L=1500):
+    lo, hi = total * rank // world, total * (rank + 1) // world
+    n = hi - lo
+    frames = synth.fixed_frames(n, L, synth.SEED_CONFIG4, first_frame=lo, device=dev)
     eng.seal_fixed(frames, L, n=n)
     frames[torch.arange(0, n, 1000, device=dev) * L + 3] ^= 1
     crc = torch.empty(n, dtype=torch.int32, device=dev)
@@ -83,51 +119,74 @@ def shard(eng, dev, n=12_500_000, L=1500, reps=10):
     fn()
     torch.cuda.synchronize()
     ok = int(valid.sum()) == n - len(range(0, n, 1000))
-    ms = timed(fn, reps, torch.cuda.current_stream())
-    algo = n * L + 5 * n
-    out = {"config": "4 (one GPU's shard): 12.5M x 1500-B device-resident", "frames": n,
-           "kernel_ms": round(ms, 4), "GiB_s": round(n * L / ms / 1e-3 / 2**30, 1),
-           "algo_GB_s": round(algo / ms / 1e-3 / 1e9, 1), "hbm_frac": round(algo / ms / 1e-3 / 8e12, 4),
-           "valid_ok": ok}
+    settle(fn)
+    med, mean = timed(fn, reps)
+    out = rates(f"4 (one GPU's shard): frames [{lo}, {hi}) of 100M x 1500 B, device-resident", n * L, n * L + 5 * n,
+                med, mean, frames=n, valid_ok=ok)
     del frames
     torch.cuda.empty_cache()
     return out
 
 
-def seal(eng, dev, n=1_000_000, L=1500, reps=20):
-    """The encode side on config 2's batch: ufc_seal_batch_fixed writes every frame's BE32
-    trailer in place (reads 1500 B, writes 4 B per frame); checked by validating afterwards."""
-    g = torch.Generator(device=dev)
-    g.manual_seed(0x5EED0004)
-    frames = torch.randint(0, 256, (n * L,), generator=g, device=dev, dtype=torch.uint8)
+def seal(eng, dev, reps, n=1_000_000, L=1500):
+    """The encode side on config 2's batch: ufc_seal_batch_fixed writes every frame's BE32 trailer
+    in place (reads 1500 B, writes 4 B per frame); checked by validating afterwards."""
+    frames = synth.fixed_frames(n, L, synth.SEED_CONFIG2, device=dev)
     fn = lambda: eng.seal_fixed(frames, L, n=n)  # noqa: E731
     fn()
     torch.cuda.synchronize()
     crc, valid = eng.crc_fixed(frames, L, n=n)
     ok = int(valid.sum()) == n
-    ms = timed(fn, reps, torch.cuda.current_stream())
-    algo = n * L + 4 * n
-    return {"config": "2 (encode side): seal 1M x 1500-B frames in place, device-resident", "frames": n,
-            "kernel_ms": round(ms, 4), "GiB_s": round(n * L / ms / 1e-3 / 2**30, 1),
-            "algo_GB_s": round(algo / ms / 1e-3 / 1e9, 1), "hbm_frac": round(algo / ms / 1e-3 / 8e12, 4),
-            "valid_after_seal": ok}
+    settle(fn)
+    med, mean = timed(fn, reps)
+    return rates("2 (encode side): seal 1M x 1500-B frames in place, device-resident", n * L, n * L + 4 * n,
+                 med, mean, frames=n, valid_after_seal=ok)
 
 
-def host(eng, n=1_000_000, L=1472, reps=5):
-    rng = np.random.default_rng(5)
+def parse(eng, dev, reps, n=1_000_000):
+    """ufc_parse_batch_varlen over n real uflow frames (data frames with datagrams, acks, syncs):
+    600 distinct frames from the codec oracle, tiled."""
+    import random
+    from oracle import codec as C
+    rng = random.Random(5)
+    base = [C.frame_write(C.random_data_frame(rng) if i % 3 == 0 else C.receive_side_data_frame(rng)
+                          if i % 3 == 1 else C.random_ack_frame(rng, 20)) for i in range(600)]
+    frames = [base[i % 600] for i in range(n)]
+    lens = np.array([len(f) for f in frames], dtype=np.int64)
+    offsets = np.zeros(n + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    blob = np.frombuffer(b"".join(base), dtype=np.uint8)
+    bo = np.zeros(601, dtype=np.int64)
+    bo[1:] = np.cumsum([len(f) for f in base])
+    data = np.concatenate([blob] * (n // 600 + 1))[: int(offsets[-1])]
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(offsets).to(dev)
+    _, valid = eng.crc_varlen(d, o)
+    infos, items, used = eng.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    cap = items.shape[0]
+    fn = lambda: eng.parse_varlen(d, o, valid, items_cap=cap)  # noqa: E731
+    settle(fn)
+    med, mean = timed(fn, reps)
+    total = int(offsets[-1])
+    k = int(used.cpu()[0])
+    return {"config": "f3: device parse (count, scan, fill) of 1M uflow frames after the gate", "frames": n,
+            "frame_bytes": total, "items": k, "ms": round(med, 4), "mean_ms": round(mean, 4),
+            "frames_per_s": round(n / med * 1e3), "GB_s_of_frame_bytes": round(total / med / 1e-3 / 1e9, 1)}
+
+
+def host(eng, reps=5, n=1_000_000, L=1472):
     res = []
     for kind in ("pinned", "pageable"):
         t = torch.empty(n * L, dtype=torch.uint8, pin_memory=(kind == "pinned"))
-        a = t.numpy()
-        a[:] = rng.integers(0, 256, size=n * L, dtype=np.uint8)
-        offsets = (np.arange(n + 1, dtype=np.uint64) * L)
-        # seal on the device (fast), copy back: the host buffer then holds valid frames
-        d = t.to("cuda")
+        d = synth.fixed_frames(n, L, synth.SEED_CONFIG2, device="cuda")
         eng.seal_fixed(d, L, n=n)
         torch.cuda.synchronize()
         t.copy_(d.cpu())
         del d
+        a = t.numpy()
         a[np.arange(0, n, 500) * L + 9] ^= 0x40
+        offsets = (np.arange(n + 1, dtype=np.uint64) * L)
         eng.validate_host_varlen(a, offsets)  # warm (staging allocation)
         times = []
         for _ in range(reps):
@@ -144,26 +203,18 @@ def host(eng, n=1_000_000, L=1472, reps=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="varlen,shard,seal,host")
+    ap.add_argument("--only", default="varlen,shard,seal,parse,host")
+    ap.add_argument("--reps", type=int, default=20)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     eng = FrameCrcEngine(0)
-    out = []
-    if "varlen" in a.only:
-        out.append(varlen(eng, dev))
-        print(json.dumps(out[-1]), flush=True)
+    for what in a.only.split(","):
+        if what == "host":
+            for r in host(eng):
+                print(json.dumps(r), flush=True)
+        else:
+            print(json.dumps(globals()[what](eng, dev, a.reps)), flush=True)
         torch.cuda.empty_cache()
-    if "shard" in a.only:
-        out.append(shard(eng, dev))
-        print(json.dumps(out[-1]), flush=True)
-    if "seal" in a.only:
-        out.append(seal(eng, dev))
-        print(json.dumps(out[-1]), flush=True)
-        torch.cuda.empty_cache()
-    if "host" in a.only:
-        for r in host(eng):
-            out.append(r)
-            print(json.dumps(r), flush=True)
     eng.close()
 
 

@@ -1,20 +1,37 @@
 #!/bin/bash
-# GPU-box measurement sequence: smoke, bench, rocprofv3 kernel-trace stats and an HBM PMC pass.
-# Every GPU step has its own time limit; the chain stops at the first failure.
+# GPU-box profiling sequence (rocprofv3, MI355X_MICROARCH.md "HBM" + "rocprofv3 PMC slots"):
+#   1. kernel trace + stats of bench.py (the config-2 validate kernel of the bench line)
+#   2. FETCH_SIZE and WRITE_SIZE of bench.py, each in its own --pmc pass
+#   3. kernel trace + stats of tools/bench_configs.py (varlen, shard, seal, parse kernels)
+#   4. FETCH_SIZE and WRITE_SIZE of tools/bench_configs.py, separate passes
+# Every step has its own time limit; the chain stops at the first failure.
+# Usage: tools/gpu_profile.sh <tag> [bench_configs --only list]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-r1}
+TAG=${1:-prof}
+ONLY=${2:-varlen,shard,seal,parse}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || { echo smoke failed; tail $OUT/smoke.log; exit 1; }
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo bench failed; tail $OUT/bench.err; exit 1; }
-cat $OUT/bench.json
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/ktrace -o run -- \
-    python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $OUT/ktrace.log 2>&1 || { echo ktrace failed; tail $OUT/ktrace.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- \
-    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/pmc_fetch.log 2>&1 || { echo pmc fetch failed; tail $OUT/pmc_fetch.log; exit 1; }
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- \
-    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/pmc_write.log 2>&1 || { echo pmc write failed; tail $OUT/pmc_write.log; exit 1; }
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2
+  shift 2
+  timeout -k 10 $secs "$@" > $OUT/$name.log 2>&1 || { echo "$name failed"; tail -20 $OUT/$name.log; exit 1; }
+  echo "$name ok"
+}
+step bench_ktrace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/bench_ktrace -o run -- \
+    python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline
+step bench_fetch 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/bench_fetch -o run -- \
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline
+step bench_write 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/bench_write -o run -- \
+    python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline
+step cfg_ktrace 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/cfg_ktrace -o run -- \
+    python3 $R/tools/bench_configs.py --only $ONLY --reps 10
+step cfg_fetch 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/cfg_fetch -o run -- \
+    python3 $R/tools/bench_configs.py --only $ONLY --reps 3
+step cfg_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/cfg_write -o run -- \
+    python3 $R/tools/bench_configs.py --only $ONLY --reps 3
+step configs 600 python3 $R/tools/bench_configs.py --reps 20
+cat $OUT/configs.log
 echo done

@@ -69,6 +69,11 @@ const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int 
 // {start (u64), len (u32), index in the run (bits 0..5) | past-the-end (bit 31)}.
 constexpr int kRunFrames = 64;
 int sort_runs(const uint64_t* offsets, bool pairs, uint64_t nframes, void* records, void* stream);
+// Sorted block-stream variable-length kernel (frame_crc_varlen2.hip): one 1024-thread workgroup per
+// CU, frames of 4..1532 B on the fast path.  pairs: (start, end) pairs with bytes_len < 2^31 - 1024.
+// Seal + pairs is not instantiated (nullptr).
+constexpr int kVarlen2Threads = 1024;
+const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

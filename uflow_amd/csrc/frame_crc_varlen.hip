@@ -89,6 +89,9 @@ constexpr int kRsrcWord3 = 0x00020000;  // gfx9-family raw buffer descriptor wor
 #define UFC_VL_AUX 2
 #endif
 constexpr int kAuxNT = UFC_VL_AUX;      // cache policy bits of the loads: 2 = nt (streaming)
+// Sorted sets take default-policy loads: a frame's first and last lines are shared with its
+// neighbours, which sorting puts in other sets; nt lines are not kept for them (config 3 FETCH_SIZE:
+// 10.0 GB with nt against 8.2 GB for 7.82 GB of frames).
 
 // ABL (tuning builds only; results meaningless): bit 0 = loads + XOR fold, no CRC; bit 1 = CRC of
 // register data, no block loads (offsets and geometry kept).
@@ -102,6 +105,7 @@ constexpr int kAuxNT = UFC_VL_AUX;      // cache policy bits of the loads: 2 = n
 template <bool SEAL, bool PAIRS, int ABL, int SCHED, int WAVES, bool SORTED>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const KernelParams p) {
   constexpr bool DYN = SCHED == kSchedClaim;
+  constexpr int kAux = SORTED ? 0 : kAuxNT;
   using OffT = typename std::conditional<SORTED, uint4, uint64_t>::type;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
   const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
@@ -209,7 +213,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
     }
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)sbase, 0, (int)kVlRecords, kRsrcWord3);
     {
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff0, 0, kAuxNT);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff0, 0, kAux);
       buf.x[0] = make_uint4(v.x, v.y, v.z, v.w);
     }
     // Every slot issues its 16-byte load, used or not: a uniform branch around a load makes
@@ -219,7 +223,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
 #pragma unroll
     for (int j = 1; j < JM; j++) {
       const uint32_t vo = (j < J) ? voff0 + 256u * j : kVlOob;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kAuxNT);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kAux);
       buf.x[j] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };

@@ -224,9 +224,6 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
   return UFC_OK;
 }
 
-// Lean variable-length kernel unless UFC_OPT_VARLEN_KERNEL = UFC_VARLEN_GENERIC (A/B measurement).
-bool lean_varlen(const ufc_ctx* ctx) { return ctx->opt[UFC_OPT_VARLEN_KERNEL] != UFC_VARLEN_GENERIC; }
-
 int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream, bool pairs = false) {
   // Claimed sets, 16 waves: measured fastest for mixed lengths (compute-heavy per set; DESIGN.md
   // section 5.2).  UFC_VARLEN_BLOCKED8: the static blocked schedule at 8 waves (A/B).
@@ -235,10 +232,10 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
     sched = ufc_dev::kSchedBlocked;
     waves = 8;
   }
-  // UFC_VARLEN_SORTED: frames sorted by block count within runs of 64 (ufc_dev::sort_runs) first.
-  // Measured (config 3): compute -9 %, but the loads lose the neighbouring frames' shared lines
-  // (loads only 1.67 -> 2.00 ms), 2.00 vs 1.88 ms overall, so it is off by default.
-  bool sorted = ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_SORTED;
+  // UFC_VARLEN_SORTED (the default): frames sorted by block count within runs of 64
+  // (ufc_dev::sort_runs) first, default-policy loads (config 3: 1.86 ms against 1.98 ms for the
+  // claimed unsorted sets).
+  bool sorted = ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_SORTED || ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_AUTO;
 #ifdef UFC_TUNING
   if (const char* ab = std::getenv("UFC_VL_ABL")) abl = std::atoi(ab);
   if (const char* sc = std::getenv("UFC_VL_SCHED")) sched = std::atoi(sc);
@@ -287,6 +284,41 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
   return UFC_OK;
 }
 
+// The sorted block-stream kernel (frame_crc_varlen2.hip, UFC_VARLEN_BLOCKSTREAM), CSR batches and pairs.
+// Pairs need the buffer below 2^31 - 1024 bytes (32-bit relative offsets); seal + pairs is not an
+// entry point.  Returns UFC_ERR_INVALID_ARG when the kernel does not apply (the caller falls back).
+int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  const void* fn = ufc_dev::varlen2_kernel_symbol(seal, pairs);
+  if (!fn || (pairs && kp.frame_len >= ((uint64_t)1 << 31) - 1024)) return UFC_ERR_INVALID_ARG;
+  kp.chain_tab = ctx->d_chain;
+  kp.nib_img = ctx->d_nib;
+  kp.G = ctx->G;
+  // Launches of < 2^31 frames (32-bit per-wave frame counts, 6-bit window indices); offsets stay
+  // absolute (relative to kp.bytes), a launch only shifts the offsets and output pointers.
+  const uint64_t chunk = (uint64_t)1 << 31;
+  const uint64_t total = kp.nframes;
+  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
+    ufc_dev::KernelParams c = kp;
+    c.nframes = std::min(chunk, total - f0);
+    c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
+    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
+    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
+    // one workgroup (16 waves) per CU; at least ~64 frames per wave
+    const uint64_t waves = ufc_dev::kVarlen2Threads / 64;
+    uint64_t blocks = (c.nframes + 64 * waves - 1) / (64 * waves);
+    if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
+    if (blocks < 1) blocks = 1;
+    void* args[] = {&c};
+    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kVarlen2Threads), args, 0, stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+  }
+  return UFC_OK;
+}
+
+// Variable-length batches: the sorted-runs kernel by default; the claimed 16-wave and blocked 8-wave
+// schedules, the block-stream kernel and the generic kernel by option.
+int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream);
+
 // Kernel configuration and mode bits for a fixed frame length: J = 256-byte blocks per frame.
 Config fixed_config(const ufc_ctx* ctx, uint64_t frame_len, int* freeze) {
   const uint64_t n = frame_len >= 4 ? frame_len - 4 : frame_len;
@@ -302,6 +334,17 @@ Config fixed_config(const ufc_ctx* ctx, uint64_t frame_len, int* freeze) {
 Config varlen_config(const ufc_ctx* ctx) {
   const int jc = ctx->opt[UFC_OPT_GENERIC_JC];
   return Config{ufc_dev::config_available(jc) ? jc : 3};
+}
+
+int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  const int opt = ctx->opt[UFC_OPT_VARLEN_KERNEL];
+  if (opt == UFC_VARLEN_BLOCKSTREAM) {
+    const int rc = launch_varlen2(ctx, seal, pairs, kp, stream);
+    if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the round-1 kernel below)
+  }
+  if (opt == UFC_VARLEN_GENERIC && !pairs)
+    return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen | (seal ? ufc_dev::kModeSeal : 0), kp, stream);
+  return launch_lean_varlen(ctx, seal, kp, stream, pairs);
 }
 
 constexpr uint64_t kMaxFrameLen = (uint64_t)1 << 30;  // per-frame limit of the 32-bit offsets math
@@ -366,7 +409,7 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
       if (value < UFC_FIXED_AUTO || value > UFC_FIXED_CLAIM16) return UFC_ERR_INVALID_ARG;
       break;
     case UFC_OPT_VARLEN_KERNEL:
-      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_BLOCKED8) return UFC_ERR_INVALID_ARG;
+      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_BLOCKSTREAM) return UFC_ERR_INVALID_ARG;
       break;
     case UFC_OPT_GENERIC_JC:
       if (value != 0 && !ufc_dev::config_available(value)) return UFC_ERR_INVALID_ARG;
@@ -420,7 +463,9 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
   if (const char* k = std::getenv("UFC_VARLEN_KERNEL"))
     ctx->opt[UFC_OPT_VARLEN_KERNEL] = std::strcmp(k, "generic") == 0 ? UFC_VARLEN_GENERIC
                                       : std::strcmp(k, "sorted") == 0 ? UFC_VARLEN_SORTED
-                                      : std::strcmp(k, "blocked8") == 0 ? UFC_VARLEN_BLOCKED8 : UFC_VARLEN_AUTO;
+                                      : std::strcmp(k, "blocked8") == 0 ? UFC_VARLEN_BLOCKED8
+                                      : std::strcmp(k, "claim16") == 0 ? UFC_VARLEN_CLAIM16
+                                      : std::strcmp(k, "blockstream") == 0 ? UFC_VARLEN_BLOCKSTREAM : UFC_VARLEN_AUTO;
   if (const char* j = std::getenv("UFC_FIXED_JC")) ctx->opt[UFC_OPT_GENERIC_JC] = std::atoi(j);
 #endif
   *out = ctx;
@@ -503,8 +548,7 @@ int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
-  if (lean_varlen(ctx)) return launch_lean_varlen(ctx, false, kp, (hipStream_t)stream);
-  return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen, kp, (hipStream_t)stream);
+  return launch_varlen_any(ctx, false, false, kp, (hipStream_t)stream);
 }
 
 int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
@@ -539,8 +583,7 @@ int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offs
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
-  if (lean_varlen(ctx)) return launch_lean_varlen(ctx, true, kp, (hipStream_t)stream);
-  return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
+  return launch_varlen_any(ctx, true, false, kp, (hipStream_t)stream);
 }
 
 static int validate_host_varlen_impl(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
@@ -625,7 +668,7 @@ static int validate_host_varlen_impl(ufc_ctx* ctx, const uint8_t* h_bytes, const
     kp.nframes = nf;
     kp.crc_out = dcrc;
     kp.valid_out = dval;
-    int rc = lean_varlen(ctx) ? launch_lean_varlen(ctx, false, kp, s) : launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen, kp, s);
+    int rc = launch_varlen_any(ctx, false, false, kp, s);
     if (rc != UFC_OK) return rc;
     if (h_crc_out && (e = hipMemcpyAsync(h_crc_out + a, dcrc, nf * 4, hipMemcpyDeviceToHost, s)) != hipSuccess)
       return hip_fail(ctx, e);
@@ -650,7 +693,7 @@ int ufc_crc_batch_pairs(ufc_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, 
   kp.crc_out = d_crc_out;
   kp.valid_out = d_valid_out;
   DeviceGuard g(ctx->device);
-  return launch_lean_varlen(ctx, false, kp, (hipStream_t)stream, true);
+  return launch_varlen_any(ctx, false, true, kp, (hipStream_t)stream);
 }
 
 static int validate_host_slots_impl(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
