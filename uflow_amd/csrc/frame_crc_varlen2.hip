@@ -63,23 +63,6 @@ __device__ __forceinline__ uint32_t g_set(uint32_t g) { return (g >> 16) & 15u; 
 constexpr uint32_t kStValid = 1u << 6, kStFirst = 1u << 7, kStMixed = 1u << 8, kStG1 = 1u << 9;
 constexpr int kStShift = 22;
 
-// Block 0 of a frame, lane with p = pad - 16 col bytes before the frame: bytes before the frame
-// become zeros, except the 4 right before it, which become G (the reference's initial ~0 folded
-// into a linear CRC).  p <= 0: the data unchanged; p >= 20: all zero.
-__device__ __forceinline__ uint4 front_fix(uint4 x, int p, uint32_t G) {
-  const uint32_t pc = (uint32_t)min(max(p, 0), 20);
-  const uint32_t s = 8u * pc;  // data bytes start at bit s of the 128-bit lane
-  const uint64_t lo = (uint64_t)x.x | ((uint64_t)x.y << 32), hi = (uint64_t)x.z | ((uint64_t)x.w << 32);
-  const uint64_t mlo = s >= 64u ? 0ull : ~0ull << s;
-  const uint64_t mhi = s >= 128u ? 0ull : (s <= 64u ? ~0ull : ~0ull << (s - 64u));
-  const int q = (int)pc - 4;  // G's first byte in the lane: -4..16
-  const uint64_t g = G;
-  const uint64_t glo = q < 0 ? (g >> ((uint32_t)(-8 * q) & 63u)) & (q == -4 ? 0ull : ~0ull) : (q < 8 ? g << (8 * q) : 0ull);
-  const uint64_t ghi = q <= 4 ? 0ull : (q < 8 ? g >> (64 - 8 * q) : (q < 16 ? g << (8 * (q - 8)) : 0ull));
-  const uint64_t rlo = (lo & mlo) | glo, rhi = (hi & mhi) | ghi;
-  return make_uint4((uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32));
-}
-
 // Stores written as inline asm (see frame_crc_dev.hpp st_u32_hidden).
 __device__ __forceinline__ void st_u8_hidden_v2(uint8_t* a, uint32_t v) {
   asm volatile("global_store_byte %0, %1, off" : : "v"(a), "v"(v));
