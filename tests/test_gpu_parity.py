@@ -392,14 +392,15 @@ def test_fixed_multi_launch(engine, frame_len, extra):
         assert np.array_equal(got, ref_crc)
 
 
-@pytest.mark.parametrize("mode", ["sorted", "blocked8", "generic", "claim16", "blockstream"])
+@pytest.mark.parametrize("mode", ["sorted", "blocked8", "generic", "claim16", "blockstream", "sorted8"])
 def test_varlen_alternate_modes(engine, mode):
     """The varlen kernel's A/B modes (ufc_ctx_set_option): run-sorted records (the default, set
     explicitly), the static blocked schedule at 8 waves, the generic kernel, the claimed unsorted
     sets, the block-stream kernel -- mixed lengths, edge lengths, seal, gapped pairs."""
     from uflow_amd import _native as N
     value = {"sorted": N.UFC_VARLEN_SORTED, "blocked8": N.UFC_VARLEN_BLOCKED8, "generic": N.UFC_VARLEN_GENERIC,
-             "claim16": N.UFC_VARLEN_CLAIM16, "blockstream": N.UFC_VARLEN_BLOCKSTREAM}[mode]
+             "claim16": N.UFC_VARLEN_CLAIM16, "blockstream": N.UFC_VARLEN_BLOCKSTREAM,
+             "sorted8": N.UFC_VARLEN_SORTED8}[mode]
     engine.set_option(N.UFC_OPT_VARLEN_KERNEL, value)
     try:
         assert engine.get_option(N.UFC_OPT_VARLEN_KERNEL) == value

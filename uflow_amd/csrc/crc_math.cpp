@@ -119,9 +119,9 @@ uint32_t host_extend(uint32_t initial_crc, const uint8_t* data, size_t len) {
   return ~reg;
 }
 
-void build_chain_table(uint32_t out[1024]) {
+void build_chain_table(uint32_t out[1024], uint64_t nbytes) {
   for (int k = 0; k < 4; k++)
-    for (int e = 0; e < 256; e++) out[k * 256 + e] = advance((uint32_t)e << (8 * k), 256);
+    for (int e = 0; e < 256; e++) out[k * 256 + e] = advance((uint32_t)e << (8 * k), nbytes);
 }
 
 void build_nibble_image(uint32_t out[8192]) {
@@ -131,6 +131,13 @@ void build_nibble_image(uint32_t out[8192]) {
       for (int e = 0; e < 16; e++)
         out[(k * 16 + e) * 64 + c] = advance((uint32_t)e << (4 * k), (uint64_t)4 * (63 - s));
   }
+}
+
+void build_nibble_image32(uint32_t out[8192]) {
+  for (int c = 0; c < 64; c++)
+    for (int k = 0; k < 8; k++)
+      for (int e = 0; e < 16; e++)
+        out[(k * 16 + e) * 64 + c] = c < 32 ? advance((uint32_t)e << (4 * k), (uint64_t)4 * (31 - c)) : 0u;
 }
 
 }  // namespace ufc

@@ -35,9 +35,11 @@ uint32_t init_prefix_word();
 uint32_t host_extend(uint32_t initial_crc, const uint8_t* data, size_t len);
 
 // Device table images (layouts documented in frame_crc.hip):
-//   chain[k*256 + e] = A^256(e << 8k)                       k = 0..3, e = 0..255   (1024 words)
+//   chain[k*256 + e] = A^nbytes(e << 8k)                    k = 0..3, e = 0..255   (1024 words)
 //   nib[(k*16 + e)*64 + c] = A^(4(63 - s))(e << 4k),  s = ((c & 31) << 1) | (c >> 5)  (8192 words)
-void build_chain_table(uint32_t out[1024]);
+//   nib32[(k*16 + e)*64 + c] = A^(4(31 - c))(e << 4k) for c < 32, 0 above (8-lane frames, 32 slots)
+void build_chain_table(uint32_t out[1024], uint64_t nbytes);
 void build_nibble_image(uint32_t out[8192]);
+void build_nibble_image32(uint32_t out[8192]);
 
 }  // namespace ufc

@@ -188,7 +188,11 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
     const uint32_t n = l32 >= 4u ? l32 - 4u : l32;
     const uint32_t J = min((n + 8u + 255u) >> 8, 15u);
     const uint32_t pad = (J * 256u - (n + 4u)) & 511u;
+#ifdef UFC_VL_UNALIGNED  // tuning experiment: byte-exact (unaligned) block loads, no realignment
+    const uint32_t dl = 0;
+#else
     const uint32_t dl = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - pad)) & 3u;
+#endif
     const bool bad = dead || l32 < 4u || J > (uint32_t)JM || a < (uint64_t)pad || rel > (1u << 20) || b + 3 > buf_end;
     m.slow = __builtin_amdgcn_ballot_w64(bad) != 0;
     m.Jset = max(max(__builtin_amdgcn_readlane((int)J, 0), __builtin_amdgcn_readlane((int)J, 16)),
@@ -274,6 +278,9 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
     // previous lane's last loaded word of block j - 1 (row_ror:1), for lane 0.
     uint32_t rp = 0;
     auto realign = [&](const uint4& w) -> uint4 {
+#ifdef UFC_VL_UNALIGNED
+      return w;
+#endif
       const uint32_t r = (uint32_t)__builtin_amdgcn_mov_dpp((int)w.w, 0x121, 0xF, 0xF, false);  // row_ror:1
       const uint32_t prev = (L.col == 0) ? rp : r;
       rp = r;

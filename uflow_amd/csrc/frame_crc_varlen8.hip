@@ -1,0 +1,394 @@
+// frame_crc_varlen8.hip -- variable-length frame-CRC kernel with 8 lanes per frame, for MI355X /
+// gfx950: BASELINE.json config 3 (10M frames of U[64,1500] B) and the receive path.
+//
+// The batched CRC gate of Frame::read (src/frame/serial/mod.rs:675-690) and the frame seal
+// (serial/mod.rs:463-470, build.rs:151-159) for frame i = bytes[offsets[i] .. offsets[i+1]) (or
+// (start, end) pairs).  Same virtual stream as the other kernels (frame_crc_dev.hpp): the frame is
+// right-aligned into J 256-byte blocks behind zeros and G.  What differs is the lane layout:
+//   * A set is 8 frames, one per 8-lane group.  Lane col of a group loads two 16-byte pieces of
+//     each block, at 16 col and 128 + 16 col, so one wave-instruction still reads 128-byte runs and
+//     a set's frame loads whole 256-byte blocks.
+//   * The two pieces are consecutive 128-byte sub-blocks of one Horner chain per slot: 32 slots
+//     (lane col holds slots 4 col + b) with the constant A^128, i.e. V_s <- A^128 V_s ^ word twice
+//     per block.  The finish is lin = XOR_s A^(4(31-s)) V_s: 32 slot words per frame instead of
+//     64, so the per-frame finish (nibble lookups, the only per-frame LDS work) costs half.  On
+//     gfx950 every integer VALU instruction is 4 cycles per wave and the lean varlen kernels are
+//     VALU-bound (SQ_ACTIVE_INST_VALU ~ SQ_INSTS_VALU with the SIMD busy all along): per-frame work
+//     -- geometry, loads, front fix, finish, results -- is shared by 8 frames instead of 4.
+//   * Sets come from run-sorted records (sort_runs, frame_crc_varlen.hip): a run of 64 frames is
+//     ordered by block count J, so a set's 8 frames mostly share J (one uniform block loop, no
+//     frozen chains); a set mixing block counts freezes the chains of its shorter frames.
+//   * Loads are default-policy raw buffer loads from one resource per wave (4-byte-aligned, the
+//     frame's window rebuilt with one v_perm per word; the lines a frame shares with its
+//     neighbours, which sort into other sets, stay in L2 for them).  Lanes wholly before their
+//     frame and blocks past it load nothing (out-of-range offsets).
+//   * Results of a run (8 sets x 8 frames) collect in one register pair per lane and leave with
+//     hidden stores once per run.  Sets with a frame the fast path cannot take (shorter than 4 B,
+//     longer than 6 blocks, at the batch edges, past its end) run byte-wise, in the same loop.
+#include "frame_crc_dev.hpp"
+
+namespace ufc_dev {
+
+namespace {
+
+constexpr int kV8Blocks = 6;               // fast path: frames of 4..1532 B
+constexpr uint32_t kV8Bias = 1024;         // lane offsets: relative to the wave's base - bias
+constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
+constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
+constexpr int kV8Aux = 0;                  // default cache policy (shared boundary lines)
+
+// Per-lane geometry of a set (one VGPR): pad [0,9), J [9,12), len >= 5 [12], dl [13,15), frame
+// index in its run [16,22), past the batch end [22].
+__device__ __forceinline__ uint32_t v8_pad(uint32_t g) { return g & 511u; }
+__device__ __forceinline__ uint32_t v8_J(uint32_t g) { return (g >> 9) & 7u; }
+__device__ __forceinline__ uint32_t v8_sel(uint32_t g) { return 0x03020100u + (4u - ((g >> 13) & 3u)) * 0x01010101u; }
+__device__ __forceinline__ uint32_t v8_orig(uint32_t g) { return (g >> 16) & 63u; }
+
+struct Lane8 {
+  const char* lds;
+  uint32_t lane, col, grp;
+  uint32_t K;    // chain-table key (as Lane::K)
+  uint32_t K2;   // nibble key: byte i = column*4 of the slot word multiplied in nibble step i
+  uint32_t rot;  // group & 3: nibble step i multiplies slot word (i + rot) & 3
+  uint32_t G;
+};
+
+__device__ __forceinline__ void init_lane8(Lane8& L, char* lds, uint32_t G) {
+  L.lds = lds;
+  L.lane = threadIdx.x & 63u;
+  L.col = L.lane & 7u;
+  L.grp = L.lane >> 3;
+  L.rot = L.grp & 3u;
+  L.G = G;
+  const uint32_t c4 = (L.lane & 31u) * 4u;
+  L.K = c4 | ((c4 + 128u) << 8) | (1u << 24);
+  uint32_t k2 = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++) k2 |= ((4u * L.col + ((i + L.rot) & 3u)) * 4u) << (8 * i);  // column = slot
+  L.K2 = k2;
+}
+
+// lin of the frame held by this 8-lane group (every lane of the group receives it).  The 32 lanes
+// of an LDS half-wave read 32 distinct slot columns in every nibble step (rotation by group).
+__device__ __forceinline__ uint32_t group_lin8(const Lane8& L, const Chains& c) {
+  const bool r1 = (L.rot & 1u) != 0, r2 = (L.rot & 2u) != 0;
+  const uint32_t a01 = r1 ? c.v1 : c.v0, a12 = r1 ? c.v2 : c.v1, a23 = r1 ? c.v3 : c.v2, a30 = r1 ? c.v0 : c.v3;
+  const uint32_t X0 = r2 ? a23 : a01, X1 = r2 ? a30 : a12, X2 = r2 ? a01 : a23, X3 = r2 ? a12 : a30;
+  uint32_t v = xor3(nib_mul<0>(L.lds, X0, L.K2), nib_mul<1>(L.lds, X1, L.K2), nib_mul<2>(L.lds, X2, L.K2)) ^
+               nib_mul<3>(L.lds, X3, L.K2);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return v;
+}
+
+__device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
+  c.v0 = chain_step(L.lds, c.v0, L.K, x.x);
+  c.v1 = chain_step(L.lds, c.v1, L.K, x.y);
+  c.v2 = chain_step(L.lds, c.v2, L.K, x.z);
+  c.v3 = chain_step(L.lds, c.v3, L.K, x.w);
+}
+
+// One 256-byte block j of a frame (pieces x0 at 16 col, x1 at 128 + 16 col, window-aligned):
+// front fix of block 0 (and of block 1's first word when G straddles into it), trailer capture on
+// the frame's last block (lane 7's last word of piece 1), two A^128 steps.  FREEZE: chains stop
+// after the frame's own J blocks.
+template <bool FREEZE>
+__device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, uint32_t pad, bool g1, bool last_any,
+                                       uint4 x0, uint4 x1, Chains& c) {
+  if (FREEZE ? (j + 1 == J) : last_any) {
+    c.tr = x1.w;
+    x1.w = (L.col == 7u) ? 0u : x1.w;
+  }
+  if (j == 0) {
+    const uint4 f0 = front_fix(x0, (int)pad - (int)(16u * L.col), L.G);
+    x1 = front_fix(x1, (int)pad - 128 - (int)(16u * L.col), L.G);
+    c.v0 = f0.x;
+    c.v1 = f0.y;
+    c.v2 = f0.z;
+    c.v3 = f0.w;
+    chain4(L, c, x1);
+    return;
+  }
+  if (j == 1 && g1) x0.x = fix_word(x0.x, 256 + (int)(16u * L.col) - (int)pad, L.G);
+  Chains n = c;
+  chain4(L, n, x0);
+  chain4(L, n, x1);
+  if (FREEZE) {
+    const bool act = j < J;
+    c.v0 = act ? n.v0 : c.v0;
+    c.v1 = act ? n.v1 : c.v1;
+    c.v2 = act ? n.v2 : c.v2;
+    c.v3 = act ? n.v3 : c.v3;
+  } else {
+    c.v0 = n.v0;
+    c.v1 = n.v1;
+    c.v2 = n.v2;
+    c.v3 = n.v3;
+  }
+}
+
+struct Set8Meta {
+  uint32_t Jset;  // max J of the set's frames
+  bool slow;      // byte path
+  bool mixed;     // block counts differ
+  bool g1;        // a frame's G straddles into block 1 (pad > 256)
+};
+
+template <int J>
+struct Buf8 {
+  uint4 x[2 * J];
+};
+
+}  // namespace
+
+// WAVES waves per workgroup (one workgroup per CU); DEPTH sets per wave in the ring (the set
+// computed plus DEPTH - 1 in flight).  p.offsets = the run-sorted records, p.offsets_csr = the
+// CSR offsets (nullptr for pairs: p.frame_len = the buffer length, relative offsets < 2^31).
+template <bool SEAL, bool PAIRS, int WAVES, int DEPTH>
+__global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
+  constexpr int JM = kV8Blocks;
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
+  Lane8 L;
+  init_lane8(L, lds, p.G);
+  const uint64_t nfr = p.nframes;
+  const uint32_t nruns = (uint32_t)((nfr + kRunFrames - 1) / kRunFrames);
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t W = gridDim.x * WAVES, w = blockIdx.x * WAVES + wid;
+  const uint32_t R0 = (uint32_t)((uint64_t)nruns * w / W), R1 = (uint32_t)((uint64_t)nruns * (w + 1) / W);
+  const uint32_t q_lo = R0 * 8u, q_end = R1 * 8u;  // this wave's sets (8 per run)
+  const uint4* rec = (const uint4*)p.offsets;
+  // The wave's base: its first frame's start (CSR offsets grow), or the buffer itself (pairs).
+  uint64_t b0 = 0;
+  if (!PAIRS && R0 < R1) {
+    const uint64_t v = *as_global<g_u64>(p.offsets_csr + (uint64_t)R0 * kRunFrames);
+    b0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
+    b0 &= ~3ull;
+  }
+  const uint8_t* base = p.bytes + b0 - kV8Bias;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)0x7FFFFFF0, 0x00020000);
+  const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets_csr + nfr);
+
+  // This group's record of set q (the same 16 bytes in the group's 8 lanes).
+  auto load_rec = [&](uint32_t q) -> uint4 {
+    const uint32_t qc = q_end > q_lo ? min(q, q_end - 1) : 0u;  // (a wave without runs reads set 0)
+    const u32x4 r = *as_global<g_u32x4>((const uint32_t*)(rec + (uint64_t)qc * 8 + L.grp));
+    return make_uint4(r.x, r.y, r.z, r.w);
+  };
+  // Geometry of set q from its record: packed per-lane geometry, block-0 piece-0 offset, meta.
+  auto geometry = [&](uint32_t q, uint4 r, uint32_t& voff0, Set8Meta& m) -> uint32_t {
+    const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
+    const uint32_t len = min(r.z, 0x40000000u);  // (longer: J > 6, the byte path)
+    const bool dead = (r.w >> 31) != 0;
+    const uint32_t J = (len + 4u + 255u) >> 8;
+    const uint32_t pad = (J * 256u - len) & 511u;
+    const uint64_t rel64 = a - b0;  // (a >= b0 for CSR; pairs: b0 = 0)
+    const uint32_t wrel = (uint32_t)rel64 + kV8Bias - pad;  // window start
+    const uint32_t dl = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - pad)) & 3u;
+    const bool bad = dead || len < 4u || J > (uint32_t)JM || a < (uint64_t)pad || a + len + 3 > buf_end ||
+                     rel64 >= (uint64_t)kV8Limit;
+    m.slow = __builtin_amdgcn_ballot_w64(bad) != 0;
+    uint32_t jmax = 0, jmin = 7;
+#pragma unroll
+    for (int g = 0; g < 8; g++) {
+      const uint32_t jg = (uint32_t)__builtin_amdgcn_readlane((int)J, 8 * g);
+      jmax = max(jmax, jg);
+      jmin = min(jmin, jg);
+    }
+    m.Jset = min(jmax, (uint32_t)JM);
+    m.mixed = jmin != jmax;
+    m.g1 = __builtin_amdgcn_ballot_w64(pad > 256u) != 0;
+    const bool live = q < q_end && !m.slow;
+    voff0 = live ? wrel + dl + 16u * L.col : kV8Oob;
+    return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (dl << 13) | ((r.w & 63u) << 16) |
+           ((dead ? 1u : 0u) << 22);
+  };
+  // The set's loads: block j's pieces at voff0 + 256 j (+ 128); pieces wholly before the frame
+  // and blocks past it are out of range.
+  auto load_set = [&](uint32_t voff0, uint32_t geo, Buf8<JM>& b) {
+    const uint32_t J = v8_J(geo), pad = v8_pad(geo), dl = (geo >> 13) & 3u;
+#pragma unroll
+    for (int j = 0; j < JM; j++) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        uint32_t vo = ((uint32_t)j < J) ? voff0 + 256u * j + 128u * h : kV8Oob;
+        if (j == 0) vo = (128u * h + 16u * L.col + 16u + dl <= pad) ? kV8Oob : vo;
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8Aux);
+        b.x[2 * j + h] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    }
+  };
+
+  // ---- results of the current run: lane (g, col = t) <- set t's frame g; qv = orig | valid << 31
+  uint32_t acc_crc = 0, acc_qv = 0;
+  auto record = [&](uint32_t t, uint32_t crc, uint32_t qv) {
+    acc_crc = (L.col == t) ? crc : acc_crc;
+    acc_qv = (L.col == t) ? qv : acc_qv;
+  };
+  auto store_run = [&](uint32_t run) {  // hidden stores (see frame_crc_dev.hpp)
+    const uint64_t f = (uint64_t)run * kRunFrames + (acc_qv & 63u);
+    if (!(acc_qv & 0x40000000u) && f < nfr) {
+      if (p.crc_out) st_u32_hidden(p.crc_out + f, acc_crc);
+      if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_qv >> 31);
+    }
+  };
+  // The result of a set (crc in every lane of a group; trailer word in its lane 7).
+  auto finish = [&](uint32_t q, uint32_t geo, const Chains& c, uint32_t voff0) {
+    const uint32_t crc = ~group_lin8(L, c);
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
+    const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
+    if (SEAL && L.col >= 4u && !((geo >> 22) & 1u)) {  // BE32 trailer: lane 4 + k writes byte k
+      const uint32_t k = L.col - 4u, dl = (geo >> 13) & 3u;
+      st_u8_hidden((uint8_t*)p.wbytes + (base - p.bytes) + (voff0 - dl - 16u * L.col + 256u * v8_J(geo) - 4u + k),
+                   crc >> (24 - 8 * k));
+    }
+    record(q & 7u, crc, v8_orig(geo) | (ok << 31) | (((geo >> 22) & 1u) << 30));
+    if ((q & 7u) == 7u) store_run(q >> 3);
+  };
+
+  // Fast set: Jset blocks (uniform), realigned pieces.
+  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf8<JM>& b, uint32_t voff0) {
+    const uint32_t J = v8_J(geo), pad = v8_pad(geo), sel = v8_sel(geo);
+    uint32_t rp = 0;  // lane 7's last loaded word of the previous block's piece 1 (for lane 0)
+    Chains c{0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < JM; j++) {
+      if ((uint32_t)j < m.Jset) {
+        const uint4 w0 = b.x[2 * j], w1 = b.x[2 * j + 1];
+        const uint32_t r1a = (uint32_t)__builtin_amdgcn_mov_dpp((int)w0.w, 0x121, 0xF, 0xF, false);  // row_ror:1
+        const uint32_t r1b = (uint32_t)__builtin_amdgcn_mov_dpp((int)w1.w, 0x121, 0xF, 0xF, false);
+        const uint32_t r9a = (uint32_t)__builtin_amdgcn_mov_dpp((int)w0.w, 0x129, 0xF, 0xF, false);  // row_ror:9
+        const uint32_t r9b = (uint32_t)__builtin_amdgcn_mov_dpp((int)w1.w, 0x129, 0xF, 0xF, false);
+        const uint32_t pa = (L.col == 0u) ? rp : r1a, pb = (L.col == 0u) ? r9a : r1b;
+        rp = r9b;
+        const uint4 x0 = make_uint4(perm(w0.x, pa, sel), perm(w0.y, w0.x, sel), perm(w0.z, w0.y, sel), perm(w0.w, w0.z, sel));
+        const uint4 x1 = make_uint4(perm(w1.x, pb, sel), perm(w1.y, w1.x, sel), perm(w1.z, w1.y, sel), perm(w1.w, w1.z, sel));
+        if (m.mixed)
+          block8<true>(L, (uint32_t)j, J, pad, m.g1, false, x0, x1, c);
+        else
+          block8<false>(L, (uint32_t)j, J, pad, m.g1, (uint32_t)j + 1 == m.Jset, x0, x1, c);
+      }
+    }
+    finish(q, geo, c, voff0);
+  };
+
+  // Byte path of set q: any lengths, loads restricted to each frame; the same result handling.
+  auto slow_set = [&](uint32_t q) {
+    const uint4 r = load_rec(q);
+    const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
+    const bool dead = (r.w >> 31) != 0;
+    const uint32_t len = dead ? 0u : r.z;
+    const FrameDesc d = make_desc(a, len);
+    uint32_t nb = 0;
+#pragma unroll
+    for (int g = 0; g < 8; g++) nb = max(nb, (uint32_t)__builtin_amdgcn_readlane(d.J, 8 * g));
+    Chains c{0u, 0u, 0u, 0u, 0u};
+    auto word = [&](int o) -> uint32_t {  // frame bytes [o, o + 4), zeros outside the frame
+      uint32_t v = 0;
+#pragma unroll 1
+      for (int k = 0; k < 4; k++) {
+        const int ob = o + k;
+        if (ob >= 0 && ob < (int)d.len) v |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
+      }
+      return v;
+    };
+#pragma unroll 1
+    for (uint32_t j = 0; j < nb; j++) {
+      const uint32_t jb = min(j, (uint32_t)d.J - 1u);
+      const int o0 = 256 * (int)jb + 16 * (int)L.col - d.pad;
+      const uint4 x0 = make_uint4(word(o0), word(o0 + 4), word(o0 + 8), word(o0 + 12));
+      const uint4 x1 = make_uint4(word(o0 + 128), word(o0 + 132), word(o0 + 136), word(o0 + 140));
+      block8<true>(L, j, (uint32_t)d.J, (uint32_t)d.pad, true, false, x0, x1, c);
+    }
+    const uint32_t geo = ((d.len >= 5u ? 1u : 0u) << 12) | ((r.w & 63u) << 16) | ((dead ? 1u : 0u) << 22);
+    const uint32_t crc = ~group_lin8(L, c);
+    const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
+    const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
+    if (SEAL && L.col == 7u && !dead && d.len >= 4u) {
+      g_u8w* wp = as_global<g_u8w>(p.wbytes + d.start + d.n);
+      wp[0] = (uint8_t)(crc >> 24);
+      wp[1] = (uint8_t)(crc >> 16);
+      wp[2] = (uint8_t)(crc >> 8);
+      wp[3] = (uint8_t)crc;
+    }
+    record(q & 7u, crc, v8_orig(geo) | (ok << 31) | ((dead ? 1u : 0u) << 30));
+    if ((q & 7u) == 7u) store_run(q >> 3);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no visible load or store stays pending
+  };
+
+  // ---- ring: set S_k in slot k % DEPTH; records DEPTH sets ahead of their geometry ----
+  static_assert(DEPTH == 2 || DEPTH == 3, "ring depth");
+  Buf8<JM> B[DEPTH];
+  uint4 O[DEPTH];
+  uint32_t GE[DEPTH], VO[DEPTH];
+  Set8Meta M[DEPTH];
+  uint32_t S = q_lo;  // the set computed next
+  // prologue: records of S .. S + 2 DEPTH - 2, geometry + loads of S .. S + DEPTH - 2
+  uint4 Rq[DEPTH];
+#pragma unroll
+  for (int i = 0; i < DEPTH; i++) Rq[i] = load_rec(S + i);
+#pragma unroll
+  for (int i = 0; i < DEPTH - 1; i++) {
+    GE[i] = geometry(S + i, Rq[i], VO[i], M[i]);
+    load_set(VO[i], GE[i], B[i]);
+    O[i] = load_rec(S + DEPTH + i);
+  }
+  O[DEPTH - 1] = Rq[DEPTH - 1];
+  stage_store<WAVES * 64>(sr, lds);
+
+  // One step: geometry + loads of set S + DEPTH - 1 (record loaded DEPTH steps ago), the record of
+  // set S + 2 DEPTH - 1, then compute set S.
+  auto step = [&](int cs, int fs) {
+    GE[fs] = geometry(S + DEPTH - 1, O[fs], VO[fs], M[fs]);
+    load_set(VO[fs], GE[fs], B[fs]);
+    O[fs] = load_rec(S + 2 * DEPTH - 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (S < q_end) {
+      if (!M[cs].slow)
+        compute(S, GE[cs], M[cs], B[cs], VO[cs]);
+      else
+        slow_set(S);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    S++;
+  };
+  if constexpr (DEPTH == 3) {
+    while (S < q_end) {
+      step(0, 2);
+      step(1, 0);
+      step(2, 1);
+    }
+  } else {
+    while (S < q_end) {
+      step(0, 1);
+      step(1, 0);
+    }
+  }
+}
+
+#define UFC_V8_INST(SEAL, PAIRS, WV, D) \
+  template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, WV, D>(const KernelParams);
+UFC_V8_INST(false, false, 8, 3) UFC_V8_INST(true, false, 8, 3) UFC_V8_INST(false, true, 8, 3) UFC_V8_INST(true, true, 8, 3)
+#ifdef UFC_TUNING
+UFC_V8_INST(false, false, 8, 2) UFC_V8_INST(false, false, 12, 2)
+#endif
+#undef UFC_V8_INST
+
+const void* varlen8_kernel_symbol(bool seal, bool pairs, int waves, int depth) {
+  if (waves == 8 && depth == 3) {
+    if (pairs)
+      return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 8, 3>
+                  : (const void*)frame_crc_varlen8_kernel<false, true, 8, 3>;
+    return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 8, 3>
+                : (const void*)frame_crc_varlen8_kernel<false, false, 8, 3>;
+  }
+#ifdef UFC_TUNING
+  if (!seal && !pairs && waves == 8 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 8, 2>;
+  if (!seal && !pairs && waves == 12 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2>;
+#endif
+  return nullptr;
+}
+
+}  // namespace ufc_dev

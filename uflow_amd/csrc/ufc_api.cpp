@@ -25,6 +25,8 @@ struct ufc_ctx {
   int ncu = 0;
   uint32_t* d_chain = nullptr;
   uint32_t* d_nib = nullptr;
+  uint32_t* d_chain128 = nullptr;  // 8-lane varlen kernel: A^128 chain tables, 32-slot nibble image
+  uint32_t* d_nib32 = nullptr;
   uint32_t G = 0;
   int last_hip_error = 0;
   // host-buffer path (ufc_validate_host_varlen): device staging, reused across calls
@@ -315,6 +317,49 @@ int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   return UFC_OK;
 }
 
+// The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): run-sorted records
+// (ufc_dev::sort_runs) into per-stream scratch, then one launch per chunk of < 2^29 frames.
+// Returns UFC_ERR_INVALID_ARG when it does not apply (pairs over a buffer of 2^31 - 2^20 bytes or
+// more: 32-bit offsets), the caller then takes the 4-lane kernel.
+int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  int waves = 8, depth = 3;
+#ifdef UFC_TUNING
+  if (const char* wv = std::getenv("UFC_V8_WAVES")) waves = std::atoi(wv);
+  if (const char* dp = std::getenv("UFC_V8_DEPTH")) depth = std::atoi(dp);
+#endif
+  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, waves, depth);
+  if (!fn || (pairs && kp.frame_len >= ((uint64_t)1 << 31) - ((uint64_t)1 << 20))) return UFC_ERR_INVALID_ARG;
+  kp.chain_tab = ctx->d_chain128;
+  kp.nib_img = ctx->d_nib32;
+  kp.G = ctx->G;
+  const uint64_t chunk = (uint64_t)1 << 29;  // (32-bit set indices: 8 per run of 64 frames)
+  const uint64_t total = kp.nframes;
+  hipError_t e;
+  void* rec = nullptr;
+  const size_t need = (size_t)((std::min(chunk, total) + 63) / 64 * 64) * 16;
+  if ((e = stream_scratch(ctx, kScratchSortRec, stream, need, &rec)) != hipSuccess) return hip_fail(ctx, e);
+  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
+    ufc_dev::KernelParams c = kp;
+    c.nframes = std::min(chunk, total - f0);
+    c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
+    if ((e = (hipError_t)ufc_dev::sort_runs(c.offsets, pairs, c.nframes, rec, stream)) != hipSuccess)
+      return hip_fail(ctx, e);
+    c.offsets_csr = pairs ? nullptr : c.offsets;
+    c.offsets = (const uint64_t*)rec;
+    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
+    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
+    // one workgroup per CU, at least one run of 64 frames per wave
+    const uint64_t nruns = (c.nframes + 63) / 64;
+    uint64_t blocks = (nruns + waves - 1) / waves;
+    if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
+    if (blocks < 1) blocks = 1;
+    void* args[] = {&c};
+    e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+  }
+  return UFC_OK;
+}
+
 // Variable-length batches: the sorted-runs kernel by default; the claimed 16-wave and blocked 8-wave
 // schedules, the block-stream kernel and the generic kernel by option.
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream);
@@ -338,6 +383,10 @@ Config varlen_config(const ufc_ctx* ctx) {
 
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
   const int opt = ctx->opt[UFC_OPT_VARLEN_KERNEL];
+  if (opt == UFC_VARLEN_SORTED8) {
+    const int rc = launch_varlen8(ctx, seal, pairs, kp, stream);
+    if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the 4-lane kernel below)
+  }
   if (opt == UFC_VARLEN_BLOCKSTREAM) {
     const int rc = launch_varlen2(ctx, seal, pairs, kp, stream);
     if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the round-1 kernel below)
@@ -409,7 +458,7 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
       if (value < UFC_FIXED_AUTO || value > UFC_FIXED_CLAIM16) return UFC_ERR_INVALID_ARG;
       break;
     case UFC_OPT_VARLEN_KERNEL:
-      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_BLOCKSTREAM) return UFC_ERR_INVALID_ARG;
+      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_SORTED8) return UFC_ERR_INVALID_ARG;
       break;
     case UFC_OPT_GENERIC_JC:
       if (value != 0 && !ufc_dev::config_available(value)) return UFC_ERR_INVALID_ARG;
@@ -439,15 +488,21 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
   if (!ctx) return UFC_ERR_NOMEM;
   ctx->device = device;
   ctx->ncu = prop.multiProcessorCount;
-  std::vector<uint32_t> chain(1024), nib(8192);
-  ufc::build_chain_table(chain.data());
+  std::vector<uint32_t> chain(1024), nib(8192), chain128(1024), nib32(8192);
+  ufc::build_chain_table(chain.data(), 256);
   ufc::build_nibble_image(nib.data());
+  ufc::build_chain_table(chain128.data(), 128);
+  ufc::build_nibble_image32(nib32.data());
   ctx->G = ufc::init_prefix_word();
   hipError_t e;
   if ((e = hipMalloc(&ctx->d_chain, chain.size() * 4)) != hipSuccess ||
       (e = hipMalloc(&ctx->d_nib, nib.size() * 4)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_chain128, chain128.size() * 4)) != hipSuccess ||
+      (e = hipMalloc(&ctx->d_nib32, nib32.size() * 4)) != hipSuccess ||
       (e = hipMemcpy(ctx->d_chain, chain.data(), chain.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMemcpy(ctx->d_nib, nib.data(), nib.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(ctx->d_chain128, chain128.data(), chain128.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
+      (e = hipMemcpy(ctx->d_nib32, nib32.data(), nib32.size() * 4, hipMemcpyHostToDevice)) != hipSuccess ||
       (e = hipMalloc(&ctx->d_ctr, (size_t)kCtrSlots * ctx->ncu * ufc_dev::kCtrWordsPerBlock * 4)) != hipSuccess ||
       (e = hipMemset(ctx->d_ctr, 0, (size_t)kCtrSlots * ctx->ncu * ufc_dev::kCtrWordsPerBlock * 4)) != hipSuccess ||
       (e = hipDeviceSynchronize()) != hipSuccess) {
@@ -465,7 +520,8 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
                                       : std::strcmp(k, "sorted") == 0 ? UFC_VARLEN_SORTED
                                       : std::strcmp(k, "blocked8") == 0 ? UFC_VARLEN_BLOCKED8
                                       : std::strcmp(k, "claim16") == 0 ? UFC_VARLEN_CLAIM16
-                                      : std::strcmp(k, "blockstream") == 0 ? UFC_VARLEN_BLOCKSTREAM : UFC_VARLEN_AUTO;
+                                      : std::strcmp(k, "blockstream") == 0 ? UFC_VARLEN_BLOCKSTREAM
+                                      : std::strcmp(k, "sorted8") == 0 ? UFC_VARLEN_SORTED8 : UFC_VARLEN_AUTO;
   if (const char* j = std::getenv("UFC_FIXED_JC")) ctx->opt[UFC_OPT_GENERIC_JC] = std::atoi(j);
 #endif
   *out = ctx;
@@ -478,6 +534,8 @@ int ufc_ctx_destroy(ufc_ctx* ctx) {
     DeviceGuard g(ctx->device >= 0 ? ctx->device : 0);
     if (ctx->d_chain) (void)hipFree(ctx->d_chain);
     if (ctx->d_nib) (void)hipFree(ctx->d_nib);
+    if (ctx->d_chain128) (void)hipFree(ctx->d_chain128);
+    if (ctx->d_nib32) (void)hipFree(ctx->d_nib32);
     if (ctx->d_ctr) (void)hipFree(ctx->d_ctr);
     for (auto& sc : ctx->scratch)
       if (sc.p) (void)hipFree(sc.p);
