@@ -127,6 +127,15 @@ int ufc_validate_host_varlen(ufc_ctx* ctx, const uint8_t* h_bytes, const uint64_
  * no host-side compaction. */
 int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
                             size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out);
+/* Asynchronous form for a receive loop that overlaps its next recvmmsg with this batch's gate
+ * (src/server/mod.rs:591-602): the H2D copies of the slots and lengths, the kernel and the D2H
+ * copies are queued on `stream` (a hipStream_t, not NULL) and the call returns.  The four host
+ * buffers must stay valid, the slots and lengths unmodified, until that work has completed
+ * (hipStreamSynchronize or an event); pinned memory (hipHostMalloc) keeps the copies asynchronous.
+ * Device staging is per (context, stream): batches on different streams may be in flight at once,
+ * from different threads (one host thread per stream).  n * slot_stride < 2^31 - 2^20. */
+int ufc_validate_host_slots_async(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
+                                  size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out, void* stream);
 /* The send side (a flush's frames laid out by the builders with zero trailers):
  * CRC of every frame on the GPU (H2D of the frames, D2H of 4 B per frame), then the BE32 trailers
  * are written into the host buffer.  h_crc_scratch: n words (receives the CRCs).  Lengths >= 4. */

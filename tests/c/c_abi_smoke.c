@@ -68,6 +68,7 @@ int main(void) {
   uint32_t scratch[4];
   CHECK(ufc_seal_host_slots(NULL, NULL, 1472, NULL, 4, scratch) == UFC_ERR_INVALID_ARG);
   CHECK(ufc_seal_host_varlen(NULL, NULL, NULL, 4, scratch) == UFC_ERR_INVALID_ARG);
+  CHECK(ufc_validate_host_slots_async(NULL, NULL, 1472, NULL, 4, scratch, NULL, NULL) == UFC_ERR_INVALID_ARG);
   CHECK(ufc_ctx_set_option(NULL, UFC_OPT_FIXED_KERNEL, UFC_FIXED_AUTO) == UFC_ERR_INVALID_ARG);
 
   /* multi-GPU layout: config 4 (100M frames over 8 GPUs) -> 12.5M frames per rank, 3 chunks */

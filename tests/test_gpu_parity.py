@@ -341,6 +341,45 @@ def test_host_slots(engine):
     assert int(valid.sum()) == n - len(range(0, n, 101))
 
 
+def test_host_slots_async(engine):
+    """ufc_validate_host_slots_async: two batches in flight on two streams from pinned buffers (the
+    receive loop's double buffering), each equal to the synchronous gate; bad arguments rejected."""
+    import torch
+    rng = np.random.default_rng(63)
+    stride = 1472
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    batches = []
+    for k, n in enumerate((4096, 1537)):
+        lens = rng.integers(0, stride + 1, size=n).astype(np.uint32)
+        lens[:3] = (0, 4, 5)
+        slots = _rand_bytes(rng, n * stride)
+        for i in range(0, n, 3):  # a third of the slots sealed (valid), the rest random
+            if lens[i] >= 4:
+                fr = bytearray(slots[i * stride:i * stride + lens[i]].tobytes())
+                oracle.frame_seal(fr)
+                slots[i * stride:i * stride + lens[i]] = np.frombuffer(bytes(fr), np.uint8)
+        h_slots = torch.from_numpy(slots).pin_memory()
+        h_lens = torch.from_numpy(lens.view(np.int32)).pin_memory()
+        crc = torch.empty(n, dtype=torch.int32).pin_memory()
+        valid = torch.empty(n, dtype=torch.uint8).pin_memory()
+        engine.validate_host_slots_async(h_slots, stride, h_lens, crc, valid, streams[k])
+        batches.append((slots, lens, crc, valid))
+    for s in streams:
+        s.synchronize()
+    for slots, lens, crc, valid in batches:
+        ref_crc, ref_valid = engine.validate_host_slots(slots, stride, lens)
+        assert np.array_equal(crc.numpy().view(np.uint32), ref_crc)
+        assert np.array_equal(valid.numpy(), ref_valid)
+        for i in range(0, len(lens), 97):
+            v, c = oracle.frame_validate(slots[i * stride:i * stride + lens[i]].tobytes())
+            assert valid[i].item() == int(v) and (crc[i].item() & 0xFFFFFFFF) == c
+    with pytest.raises(ValueError):  # device tensors are not host buffers
+        engine.validate_host_slots_async(h_slots.cuda(), stride, h_lens, crc, valid, streams[0])
+    from uflow_amd import _native as N
+    assert N.lib().ufc_validate_host_slots_async(engine._ctx, h_slots.data_ptr(), stride, h_lens.data_ptr(), 4,
+                                                 crc.data_ptr(), valid.data_ptr(), None) == N.UFC_ERR_INVALID_ARG
+
+
 def test_seal_host_varlen(engine):
     """Send-side batch seal of builder output (zero trailers) in host memory == per-frame seal."""
     from uflow_amd.frame import DataFrameBuilder, Datagram

@@ -43,3 +43,18 @@ def test_stream_cpu_gate():
 def test_stream_gpu_gate():
     n = 200_000
     _check_stream(_run(["--gate", "gpu", "--frames", str(n), "--corrupt-every", "997"]), n, 997)
+
+
+def test_stream_inline_cpu_gate():
+    """Inline receive loops (receive + gate + parse per thread, server/mod.rs:591-602) on 2 threads."""
+    n = 100_000
+    _check_stream(_run(["--gate", "cpu", "--rx-threads", "2", "--frames", str(n), "--corrupt-every", "997"]), n, 997)
+
+
+@pytest.mark.gpu
+def test_stream_inline_gpu_gate():
+    """The same with the asynchronous GPU gate overlapped with the next receive."""
+    n = 200_000
+    j = _run(["--gate", "gpu", "--rx-threads", "2", "--frames", str(n), "--corrupt-every", "997"])
+    assert j["failed_threads"] == 0
+    _check_stream(j, n, 997)

@@ -16,6 +16,12 @@
 //                 --send-seal cpu|gpu: the sender builds every flush's frames with zero trailers and
 //                 seals them in one batch (per frame on the CPU, or ufc_seal_host_slots on the GPU)
 //                 before sendmmsg, the batched form of emit.rs:114-125 + build.rs:151-159.
+//   --rx-threads R   the server loop of server/mod.rs:591-602 (receive, gate, handle in one thread)
+//                 on R threads, each with its own socket (port + r) fed by its own sender: per
+//                 batch the thread receives into one of two pinned slot buffers; with the GPU gate
+//                 it queues the batch's gate (ufc_validate_host_slots_async) and, while that runs,
+//                 parses and checks the previous batch, then receives the next; with --gate cpu it
+//                 gates each frame itself (ufc_frame_validate) before parsing.
 // Output: one JSON line (frames/s and GB/s of frame bytes received, gated and parsed).
 #include <arpa/inet.h>
 #include <hip/hip_runtime.h>
@@ -114,6 +120,8 @@ struct Args {
   uint64_t corrupt_every = 0;  // flip one bit in every k-th frame (must be rejected)
   bool verify = true;
   int send_seal = 0;  // 0: frames built once and re-sent; 1: built per flush, sealed on the CPU; 2: ... on the GPU
+  int rx_threads = 0;  // > 0: the inline receive loop on that many threads (run_stream_inline)
+  int tx_per_rx = 1;   // sender threads per receive thread (inline mode)
 };
 
 // ---------------- config 1: echo plumbing ----------------
@@ -341,7 +349,6 @@ int run_stream(const Args& a) {
   double t_gate = 0;
   std::thread worker([&] {
     std::vector<ufc_item> items(UFC_DATA_FRAME_MAX_DATAGRAM_COUNT);
-    std::vector<uint8_t> expect(kFragment);
     for (;;) {
       int k;
       {
@@ -377,8 +384,9 @@ int run_stream(const Args& a) {
             n_payload_bad++;
             continue;
           }
-          for (size_t j = 0; j < kFragment; j++) expect[j] = payload_byte(c, p, j);
-          if (memcmp(f + items[0].data_offset, expect.data(), kFragment) != 0) n_payload_bad++;
+          if (memcmp(f + items[0].data_offset, ring.data() + (size_t)(seq % kRing) * kFrame + items[0].data_offset,
+                     kFragment) != 0)
+            n_payload_bad++;
         }
       }
       std::lock_guard<std::mutex> l(mu);
@@ -472,6 +480,229 @@ int run_stream(const Args& a) {
   return (n_payload_bad == 0 && received > 0) ? 0 : 1;
 }
 
+// ---------------- config 5, inline receive loops on R threads ----------------
+struct LaneStats {
+  uint64_t received = 0, valid = 0, invalid = 0, parsed = 0, payload_bad = 0, bytes = 0;
+  double t_first = 0, t_last = 0, t_gate = 0;
+};
+
+int run_stream_inline(const Args& a) {
+  const int R = a.rx_threads;
+  const size_t B = (size_t)a.batch;
+  const uint32_t kRing = 8192;
+  std::vector<uint8_t> ring((size_t)kRing * kFrame);
+  for (uint32_t s = 0; s < kRing; s++) build_stream_frame(ring.data() + (size_t)s * kFrame, s, true);
+  std::vector<LaneStats> st(R);
+  std::vector<std::thread> threads;
+  std::atomic<int> senders_done{0};
+  std::atomic<int> failed{0};
+  std::vector<int> rx(R);
+  int rcvbuf = 0;
+  for (int r = 0; r < R; r++) {
+    rx[r] = udp_socket((uint16_t)(a.port + r), true, 64 << 20);
+    set_timeout(rx[r], 300);
+    socklen_t sl = sizeof(rcvbuf);
+    getsockopt(rx[r], SOL_SOCKET, SO_RCVBUF, &rcvbuf, &sl);
+  }
+  const int TX = R * std::max(1, a.tx_per_rx);
+  for (int t = 0; t < TX; t++) {
+    // sender t: frames [F t / TX, F (t+1) / TX) to port + t % R
+    threads.emplace_back([&, t] {
+      const int tx = udp_socket(0, false, 0);
+      const sockaddr_in to = loopback((uint16_t)(a.port + t % R));
+      const uint64_t lo = a.frames * t / TX, hi = a.frames * (t + 1) / TX;
+      const int M = 64;
+      std::vector<mmsghdr> msgs(M);
+      std::vector<iovec> iov(M);
+      std::vector<uint8_t> scratch((size_t)M * kFrame);
+      for (uint64_t s = lo; s < hi;) {
+        const int m = (int)std::min<uint64_t>(M, hi - s);
+        for (int i = 0; i < m; i++) {
+          const uint64_t q = s + i;
+          uint8_t* f = ring.data() + (size_t)(q % kRing) * kFrame;
+          if (a.corrupt_every && q % a.corrupt_every == a.corrupt_every - 1) {
+            memcpy(scratch.data() + (size_t)i * kFrame, f, kFrame);
+            f = scratch.data() + (size_t)i * kFrame;
+            f[100 + q % 1000] ^= 0x10;
+          }
+          iov[i].iov_base = f;
+          iov[i].iov_len = kFrame;
+          msgs[i].msg_hdr = msghdr{};
+          msgs[i].msg_hdr.msg_name = (void*)&to;
+          msgs[i].msg_hdr.msg_namelen = sizeof(to);
+          msgs[i].msg_hdr.msg_iov = &iov[i];
+          msgs[i].msg_hdr.msg_iovlen = 1;
+        }
+        const int k = sendmmsg(tx, msgs.data(), m, 0);
+        if (k > 0) s += (uint64_t)k;
+      }
+      close(tx);
+      senders_done++;
+    });
+  }
+  for (int r = 0; r < R; r++) {
+    // receiver r: receive, gate, parse + check, in one thread
+    threads.emplace_back([&, r] {
+      LaneStats& S = st[r];
+      ufc_ctx* ctx = nullptr;
+      hipStream_t streams[2] = {nullptr, nullptr};
+      struct Buf {
+        uint8_t* slots = nullptr;
+        uint32_t* lens = nullptr;
+        uint32_t* crc = nullptr;
+        uint8_t* valid = nullptr;
+        size_t n = 0;
+      } bufs[2];
+      auto fail = [&](const char* what) {
+        fprintf(stderr, "receiver %d: %s\n", r, what);
+        failed++;
+      };
+      if (a.gpu) {
+        if (ufc_ctx_create(&ctx, 0) != UFC_OK) return fail("ufc_ctx_create");
+        for (int k = 0; k < 2; k++) {
+          if (hipStreamCreateWithFlags(&streams[k], hipStreamNonBlocking) != hipSuccess ||
+              hipHostMalloc((void**)&bufs[k].slots, B * kFrame, hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&bufs[k].lens, B * 4, hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&bufs[k].crc, B * 4, hipHostMallocDefault) != hipSuccess ||
+              hipHostMalloc((void**)&bufs[k].valid, B, hipHostMallocDefault) != hipSuccess)
+            return fail("pinned buffers");
+        }
+      } else {
+        for (int k = 0; k < 2; k++) {
+          bufs[k].slots = (uint8_t*)malloc(B * kFrame);
+          bufs[k].lens = (uint32_t*)malloc(B * 4);
+          bufs[k].crc = (uint32_t*)malloc(B * 4);
+          bufs[k].valid = (uint8_t*)malloc(B);
+        }
+      }
+      std::vector<ufc_item> items(UFC_DATA_FRAME_MAX_DATAGRAM_COUNT);
+      std::vector<mmsghdr> msgs(B);
+      std::vector<iovec> iov(B);
+      // parse + payload check of a gated batch (the rest of Frame::read and the application)
+      auto handle = [&](const Buf& b) {
+        for (size_t i = 0; i < b.n; i++) {
+          const uint8_t* f = b.slots + i * kFrame;
+          S.bytes += b.lens[i];
+          if (!b.valid[i]) {
+            S.invalid++;
+            continue;
+          }
+          S.valid++;
+          ufc_frame_info info;
+          if (ufc_frame_parse(f, b.lens[i], 1, &info, items.data(), items.size()) != 1) continue;
+          S.parsed++;
+          if (a.verify && info.kind == UFC_FRAME_DATA && info.item_count == 1) {
+            const uint32_t seq = info.f[0], c = seq % kChannels, p = seq / kChannels;
+            if (items[0].channel_id != c || items[0].id != (p & 0xFFFFF) || items[0].data_len != kFragment ||
+                memcmp(f + items[0].data_offset, ring.data() + (size_t)(seq % kRing) * kFrame + items[0].data_offset,
+                       kFragment) != 0)
+              S.payload_bad++;
+          }
+        }
+      };
+      int cur = 0, pending = -1;
+      bool idle = false;
+      while (!idle) {
+        Buf& b = bufs[cur];
+        b.n = 0;
+        while (b.n < B) {
+          const size_t want = B - b.n;
+          for (size_t i = 0; i < want; i++) {
+            iov[i].iov_base = b.slots + (b.n + i) * kFrame;
+            iov[i].iov_len = kFrame;
+            msgs[i].msg_hdr = msghdr{};
+            msgs[i].msg_hdr.msg_iov = &iov[i];
+            msgs[i].msg_hdr.msg_iovlen = 1;
+          }
+          const int k = recvmmsg(rx[r], msgs.data(), (unsigned)want, MSG_WAITFORONE, nullptr);
+          if (k <= 0) {  // 300 ms without a datagram
+            if (senders_done.load() == TX) {
+              idle = true;
+              break;
+            }
+            if (S.received == 0) continue;
+            break;
+          }
+          if (S.received == 0) S.t_first = now_s();
+          for (int i = 0; i < k; i++) b.lens[b.n + i] = msgs[i].msg_len;
+          b.n += (size_t)k;
+          S.received += (uint64_t)k;
+          S.t_last = now_s();
+        }
+        if (a.gpu) {
+          const double t0 = now_s();
+          if (b.n && ufc_validate_host_slots_async(ctx, b.slots, kFrame, b.lens, b.n, b.crc, b.valid, streams[cur]) != UFC_OK)
+            return fail("ufc_validate_host_slots_async");
+          if (pending >= 0) {
+            if (hipStreamSynchronize(streams[pending]) != hipSuccess) return fail("hipStreamSynchronize");
+            S.t_gate += now_s() - t0;  // (queueing + waiting: the gate's cost to this thread)
+            handle(bufs[pending]);
+          } else {
+            S.t_gate += now_s() - t0;
+          }
+          pending = b.n ? cur : -1;
+          cur ^= 1;
+        } else {
+          const double t0 = now_s();
+          for (size_t i = 0; i < b.n; i++) b.valid[i] = (uint8_t)ufc_frame_validate(b.slots + i * kFrame, b.lens[i]);
+          S.t_gate += now_s() - t0;
+          handle(b);
+        }
+      }
+      if (pending >= 0) {
+        if (hipStreamSynchronize(streams[pending]) != hipSuccess) return fail("hipStreamSynchronize");
+        handle(bufs[pending]);
+      }
+      for (int k = 0; k < 2; k++) {
+        if (a.gpu) {
+          (void)hipHostFree(bufs[k].slots);
+          (void)hipHostFree(bufs[k].lens);
+          (void)hipHostFree(bufs[k].crc);
+          (void)hipHostFree(bufs[k].valid);
+          (void)hipStreamDestroy(streams[k]);
+        } else {
+          free(bufs[k].slots);
+          free(bufs[k].lens);
+          free(bufs[k].crc);
+          free(bufs[k].valid);
+        }
+      }
+      if (ctx) ufc_ctx_destroy(ctx);
+    });
+  }
+  for (auto& t : threads) t.join();
+  for (int r = 0; r < R; r++) close(rx[r]);
+  LaneStats T;
+  T.t_first = 1e300;
+  double gate_max = 0;
+  for (const LaneStats& S : st) {
+    T.received += S.received;
+    T.valid += S.valid;
+    T.invalid += S.invalid;
+    T.parsed += S.parsed;
+    T.payload_bad += S.payload_bad;
+    T.bytes += S.bytes;
+    if (S.received) {
+      T.t_first = std::min(T.t_first, S.t_first);
+      T.t_last = std::max(T.t_last, S.t_last);
+    }
+    T.t_gate += S.t_gate;
+    gate_max = std::max(gate_max, S.t_gate);
+  }
+  const double span = std::max(T.t_last - T.t_first, 1e-9);
+  printf("{\"config\": \"5: ideal_transfer-style loopback at saturation, inline receive loops (receive + %s gate + "
+         "parse + payload check per thread)\", \"rx_threads\": %d, \"frame_bytes\": %zu, \"sent\": %llu, "
+         "\"received\": %llu, \"valid\": %llu, \"invalid\": %llu, \"parsed\": %llu, \"payload_mismatch\": %llu, "
+         "\"receive_seconds\": %.4f, \"frames_per_s\": %.0f, \"GB_s\": %.3f, \"gate_thread_seconds\": %.4f, "
+         "\"gate_share_of_thread_time\": %.3f, \"batch\": %d, \"failed_threads\": %d, \"tx_threads\": %d, "
+         "\"so_rcvbuf\": %d}\n",
+         a.gpu ? "GPU (ufc_validate_host_slots_async, overlapped with the next receive)" : "CPU (ufc_frame_validate)", R,
+         kFrame, (unsigned long long)a.frames, (unsigned long long)T.received, (unsigned long long)T.valid,
+         (unsigned long long)T.invalid, (unsigned long long)T.parsed, (unsigned long long)T.payload_bad, span,
+         T.received / span, T.bytes / span / 1e9, T.t_gate, T.t_gate / (span * R), a.batch, failed.load(), TX, rcvbuf);
+  return (T.payload_bad == 0 && T.received > 0 && failed.load() == 0) ? 0 : 1;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -486,15 +717,18 @@ int main(int argc, char** argv) {
     else if (s == "--port") a.port = (uint16_t)atoi(next());
     else if (s == "--corrupt-every") a.corrupt_every = strtoull(next(), nullptr, 10);
     else if (s == "--no-verify") a.verify = false;
+    else if (s == "--rx-threads") a.rx_threads = atoi(next());
+    else if (s == "--tx-per-rx") a.tx_per_rx = atoi(next());
     else if (s == "--send-seal") {
       const std::string v = next();
       a.send_seal = v == "gpu" ? 2 : v == "cpu" ? 1 : 0;
     }
     else {
       fprintf(stderr, "usage: %s [--echo] [--gate gpu|cpu] [--frames N] [--batch B] [--port P] "
-                      "[--corrupt-every K] [--no-verify] [--send-seal none|cpu|gpu]\n", argv[0]);
+                      "[--corrupt-every K] [--no-verify] [--send-seal none|cpu|gpu] [--rx-threads R]\n", argv[0]);
       return 2;
     }
   }
-  return a.echo ? run_echo(a) : run_stream(a);
+  if (a.echo) return run_echo(a);
+  return a.rx_threads > 0 ? run_stream_inline(a) : run_stream(a);
 }

@@ -182,6 +182,22 @@ class FrameCrcEngine:
                                             crc.ctypes.data, valid.ctypes.data), "ufc_validate_host_slots")
         return crc, valid
 
+    def validate_host_slots_async(self, slots, slot_stride: int, lens, crc_out, valid_out, stream):
+        """Queue the slots gate on `stream` (torch.cuda.Stream) and return at once: slots (uint8),
+        lens (int32) and the outputs crc_out (int32[n]) / valid_out (uint8[n]) are host
+        torch tensors, ideally pinned, that must stay alive and unmodified until the stream is done."""
+        n = lens.numel()
+        need = {"slots": (slots, torch.uint8, (n - 1) * slot_stride if n else 0), "lens": (lens, torch.int32, n),
+                "crc_out": (crc_out, torch.int32, n), "valid_out": (valid_out, torch.uint8, n)}
+        for name, (t, dt, m) in need.items():
+            if not isinstance(t, torch.Tensor) or t.is_cuda or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous host tensor")
+            if t.dtype != dt or t.numel() < m:
+                raise ValueError(f"{name} must be {dt} with at least {m} elements")
+        check(lib().ufc_validate_host_slots_async(self._ctx, slots.data_ptr(), slot_stride, lens.data_ptr(), n,
+                                                  crc_out.data_ptr(), valid_out.data_ptr(), stream.cuda_stream),
+              "ufc_validate_host_slots_async")
+
     def validate_host_varlen(self, data: np.ndarray, offsets: np.ndarray):
         """numpy uint8 bytes + uint64/int64 offsets in host memory -> (crc uint32[n], valid uint8[n])."""
         data = np.ascontiguousarray(data, dtype=np.uint8)

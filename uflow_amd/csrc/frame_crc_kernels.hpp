@@ -79,6 +79,9 @@ const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // A^128 chain tables and the 32-slot nibble image.  waves/depth: 8/3 (product); others in tuning
 // builds.  Pairs need the buffer below 2^31 - 2^20 bytes (32-bit offsets from the buffer).
 const void* varlen8_kernel_symbol(bool seal, bool pairs, int waves, int depth);
+// Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride
+// + lens[i] (ufc_validate_host_slots_async).
+int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

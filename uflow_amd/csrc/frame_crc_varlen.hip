@@ -554,6 +554,23 @@ __global__ __launch_bounds__(256) void sort_runs_kernel(const uint64_t* offsets,
                                             lane | (live ? 0u : 0x80000000u));
 }
 
+__global__ __launch_bounds__(256) void slots_to_pairs_kernel(const uint32_t* lens, uint64_t stride, uint64_t n,
+                                                              uint64_t* pairs) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const uint64_t a = i * stride;
+    pairs[2 * i] = a;
+    pairs[2 * i + 1] = a + lens[i];
+  }
+}
+
+int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(slots_to_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     d_lens, stride, n, d_pairs);
+  return (int)hipGetLastError();
+}
+
 int sort_runs(const uint64_t* offsets, bool pairs, uint64_t nframes, void* records, void* stream) {
   const uint64_t nruns = (nframes + kRunFrames - 1) / kRunFrames;
   if (nruns == 0) return 0;

@@ -372,7 +372,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, WV, D>(const KernelParams);
 UFC_V8_INST(false, false, 8, 3) UFC_V8_INST(true, false, 8, 3) UFC_V8_INST(false, true, 8, 3) UFC_V8_INST(true, true, 8, 3)
 #ifdef UFC_TUNING
-UFC_V8_INST(false, false, 8, 2) UFC_V8_INST(false, false, 12, 2)
+UFC_V8_INST(false, false, 8, 2) UFC_V8_INST(false, false, 10, 2) UFC_V8_INST(false, false, 12, 2)
+UFC_V8_INST(false, false, 14, 2) UFC_V8_INST(false, false, 16, 2)
 #endif
 #undef UFC_V8_INST
 
@@ -386,7 +387,10 @@ const void* varlen8_kernel_symbol(bool seal, bool pairs, int waves, int depth) {
   }
 #ifdef UFC_TUNING
   if (!seal && !pairs && waves == 8 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 8, 2>;
+  if (!seal && !pairs && waves == 10 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 10, 2>;
   if (!seal && !pairs && waves == 12 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2>;
+  if (!seal && !pairs && waves == 14 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 14, 2>;
+  if (!seal && !pairs && waves == 16 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 16, 2>;
 #endif
   return nullptr;
 }

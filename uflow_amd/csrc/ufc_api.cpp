@@ -63,7 +63,7 @@ constexpr uint32_t kCtrSlots = 64;
 
 namespace {
 
-enum ScratchKind { kScratchParse = 0, kScratchSortRec = 1 };
+enum ScratchKind { kScratchParse = 0, kScratchSortRec = 1, kScratchAsyncSlots = 2 };
 
 // The (kind, stream) scratch buffer of at least `need` bytes.  Growing waits for the work already
 // queued on that stream (the only user of the old buffer) before freeing it.
@@ -828,6 +828,43 @@ static int validate_host_slots_impl(ufc_ctx* ctx, const uint8_t* h_slots, size_t
   return UFC_OK;
 }
 
+// Staging of one asynchronous slots batch, in the (ctx, stream) scratch: the slots' bytes, the
+// lengths, the pairs, the CRC words and the valid bytes, each 256-byte aligned.
+static int validate_host_slots_async_impl(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride,
+                                          const uint32_t* h_lens, size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out,
+                                          hipStream_t stream) {
+  if (!ctx || !stream) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;
+  if (!h_slots || !h_lens || slot_stride == 0 || (!h_crc_out && !h_valid_out)) return UFC_ERR_INVALID_ARG;
+  if (n > (((size_t)1 << 31) - ((size_t)1 << 20)) / slot_stride) return UFC_ERR_INVALID_ARG;
+  for (size_t i = 0; i < n; i++)
+    if (h_lens[i] > slot_stride) return UFC_ERR_INVALID_ARG;
+  auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  const size_t bytes = (n - 1) * slot_stride + h_lens[n - 1];  // the slab may end at the last datagram
+  const size_t o_lens = up(bytes + 64), o_pairs = o_lens + up(4 * n), o_crc = o_pairs + up(16 * n),
+               o_valid = o_crc + up(4 * n), need = o_valid + up(n);
+  void* sp = nullptr;
+  hipError_t e;
+  if ((e = stream_scratch(ctx, kScratchAsyncSlots, stream, need, &sp)) != hipSuccess) return hip_fail(ctx, e);
+  uint8_t* s = (uint8_t*)sp;
+  uint32_t* d_lens = (uint32_t*)(s + o_lens);
+  uint64_t* d_pairs = (uint64_t*)(s + o_pairs);
+  uint32_t* d_crc = (uint32_t*)(s + o_crc);
+  uint8_t* d_valid = s + o_valid;
+  if ((e = hipMemcpyAsync(s, h_slots, bytes, hipMemcpyHostToDevice, stream)) != hipSuccess ||
+      (e = hipMemcpyAsync(d_lens, h_lens, 4 * n, hipMemcpyHostToDevice, stream)) != hipSuccess)
+    return hip_fail(ctx, e);
+  if ((e = (hipError_t)ufc_dev::slots_to_pairs(d_lens, slot_stride, n, d_pairs, stream)) != hipSuccess)
+    return hip_fail(ctx, e);
+  const int rc = ufc_crc_batch_pairs(ctx, s, bytes, d_pairs, n, d_crc, d_valid, stream);
+  if (rc != UFC_OK) return rc;
+  if (h_crc_out && (e = hipMemcpyAsync(h_crc_out, d_crc, 4 * n, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(ctx, e);
+  if (h_valid_out && (e = hipMemcpyAsync(h_valid_out, d_valid, n, hipMemcpyDeviceToHost, stream)) != hipSuccess)
+    return hip_fail(ctx, e);
+  return UFC_OK;
+}
+
 // After a failure part-way through a host-buffer call, copies of earlier chunks may still be
 // queued on the context's streams (reading the caller's frames, writing its outputs): wait for
 // them before returning, so that nothing touches the caller's buffers after the call.
@@ -848,6 +885,16 @@ int ufc_validate_host_slots(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_st
                             size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out) {
   DeviceGuard g(ctx ? ctx->device : 0);
   return drain_on_error(ctx, validate_host_slots_impl(ctx, h_slots, slot_stride, h_lens, n, h_crc_out, h_valid_out));
+}
+
+int ufc_validate_host_slots_async(ufc_ctx* ctx, const uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens,
+                                  size_t n, uint32_t* h_crc_out, uint8_t* h_valid_out, void* stream) {
+  DeviceGuard g(ctx ? ctx->device : 0);
+  const int rc = validate_host_slots_async_impl(ctx, h_slots, slot_stride, h_lens, n, h_crc_out, h_valid_out,
+                                                (hipStream_t)stream);
+  // on error, nothing queued by this call may still touch the caller's buffers
+  if (rc != UFC_OK && ctx && stream) (void)hipStreamSynchronize((hipStream_t)stream);
+  return rc;
 }
 
 namespace {
