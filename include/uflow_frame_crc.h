@@ -86,7 +86,7 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 #define UFC_FIXED_GENERIC 1      /*   the generic kernel */
 #define UFC_FIXED_CLAIM16 2      /*   lean kernel, claimed schedule at 16 waves (round-1 default) */
 #define UFC_OPT_VARLEN_KERNEL 1  /* CSR / pairs batches: */
-#define UFC_VARLEN_AUTO 0        /*   the default (currently UFC_VARLEN_SORTED) */
+#define UFC_VARLEN_AUTO 0        /*   the default: UFC_VARLEN_SORTED8 (else UFC_VARLEN_SORTED) */
 #define UFC_VARLEN_GENERIC 1     /*   the generic kernel */
 #define UFC_VARLEN_SORTED 2      /*   round-1 kernel on frames sorted by block count within runs of 64 */
 #define UFC_VARLEN_BLOCKED8 3    /*   round-1 kernel, static blocked schedule at 8 waves */

@@ -9,7 +9,7 @@ port=31000
 for th in ${THREADS:-1 2 4 8}; do
   for g in cpu gpu; do
     port=$((port + 20))
-    timeout -k 10 120 $B --gate $g --rx-threads $th --frames ${FRAMES:-2000000} --corrupt-every 997 --port $port \
+    timeout -k 10 120 $B --gate $g --rx-threads $th --tx-per-rx ${TXR:-2} --frames ${FRAMES:-2000000} --corrupt-every 997 --port $port \
       >> $OUT/config5.jsonl 2>> $OUT/config5.err || { echo "run $g x$th failed"; tail -5 $OUT/config5.err; exit 1; }
   done
 done

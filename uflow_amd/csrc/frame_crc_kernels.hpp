@@ -76,7 +76,7 @@ constexpr int kVarlen2Threads = 1024;
 const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // Sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): 8-frame sets from the
 // run-sorted records (p.offsets = records, p.offsets_csr = the CSR offsets or nullptr for pairs),
-// A^128 chain tables and the 32-slot nibble image.  waves/depth: 8/3 (product); others in tuning
+// A^128 chain tables and the 32-slot nibble image.  waves/depth: 12/2 (product); others in tuning
 // builds.  Pairs need the buffer below 2^31 - 2^20 bytes (32-bit offsets from the buffer).
 const void* varlen8_kernel_symbol(bool seal, bool pairs, int waves, int depth);
 // Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride

@@ -238,6 +238,7 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
   // (ufc_dev::sort_runs) first, default-policy loads (config 3: 1.86 ms against 1.98 ms for the
   // claimed unsorted sets).
   bool sorted = ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_SORTED || ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_AUTO;
+  // (AUTO lands here only when the 8-lane kernel does not apply)
 #ifdef UFC_TUNING
   if (const char* ab = std::getenv("UFC_VL_ABL")) abl = std::atoi(ab);
   if (const char* sc = std::getenv("UFC_VL_SCHED")) sched = std::atoi(sc);
@@ -322,7 +323,7 @@ int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
 // Returns UFC_ERR_INVALID_ARG when it does not apply (pairs over a buffer of 2^31 - 2^20 bytes or
 // more: 32-bit offsets), the caller then takes the 4-lane kernel.
 int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  int waves = 8, depth = 3;
+  int waves = 12, depth = 2;
 #ifdef UFC_TUNING
   if (const char* wv = std::getenv("UFC_V8_WAVES")) waves = std::atoi(wv);
   if (const char* dp = std::getenv("UFC_V8_DEPTH")) depth = std::atoi(dp);
@@ -383,7 +384,7 @@ Config varlen_config(const ufc_ctx* ctx) {
 
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
   const int opt = ctx->opt[UFC_OPT_VARLEN_KERNEL];
-  if (opt == UFC_VARLEN_SORTED8) {
+  if (opt == UFC_VARLEN_SORTED8 || opt == UFC_VARLEN_AUTO) {
     const int rc = launch_varlen8(ctx, seal, pairs, kp, stream);
     if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the 4-lane kernel below)
   }
