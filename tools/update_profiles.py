@@ -1,6 +1,9 @@
-"""Copy a tools/gpu_profile.sh run (gpurun_out/<tag>/) into profiles/ under a round prefix and
-regenerate profiles/pmc_traffic.json (the HBM bytes per validate launch that bench.py reports
-as roofline.traffic).  Usage: python tools/update_profiles.py <tag> <prefix>, e.g. r1c r1."""
+"""Copy a tools/gpu_profile.sh run (gpurun_out/<tag>/) into profiles/ under a round prefix, write a
+per-kernel summary (<prefix>_kernels.json: average duration from the kernel trace, FETCH_SIZE and
+WRITE_SIZE bytes per dispatch from the separate --pmc passes) and regenerate profiles/pmc_traffic.json
+(the HBM bytes per validate launch that bench.py reports as roofline.traffic).
+Usage: python tools/update_profiles.py <tag> <prefix>, e.g. r2prof r2."""
+import csv
 import json
 import os
 import shutil
@@ -10,20 +13,80 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 from pmc_summary import summarise  # noqa: E402
 
-KERNEL = "fixed_kernel<6, false"
+BENCH_KERNEL = "fixed_kernel<6, false"
+# kernels of tools/bench_configs.py --only varlen,shard,seal,parse (name substrings)
+CFG_KERNELS = {
+    "varlen (config 3): 8-lane sorted-runs kernel": "frame_crc_varlen8_kernel<false, false",
+    "varlen (config 3): its sort pre-pass": "sort_runs_kernel<false>",
+    "seal (config 2 encode side)": "fixed_kernel<6, true",
+    "validate, fixed 1500 B (config 2 in bench; config-4 shard in bench_configs)": "fixed_kernel<6, false",
+    "parse: count": "parse_count",
+    "parse: fill": "parse_fill",
+}
+
+
+def kernel_stats(path):
+    out = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            out[r["Name"]] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
+                              "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3}
+    return out
+
+
+def pick(stats, sub):
+    hits = {k: v for k, v in stats.items() if sub in k}
+    return next(iter(hits.items())) if len(hits) == 1 else (None, None)
+
+
+def last_json(path):
+    with open(path) as f:
+        lines = [l for l in f if l.startswith("{")]
+    return json.loads(lines[-1])
 
 
 def main():
     tag, prefix = sys.argv[1], sys.argv[2]
     src = os.path.join(REPO, "gpurun_out", tag)
     dst = os.path.join(REPO, "profiles")
-    shutil.copy(os.path.join(src, "ktrace", "run_kernel_stats.csv"), os.path.join(dst, f"{prefix}_kernel_stats.csv"))
-    shutil.copy(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), os.path.join(dst, f"{prefix}_pmc_fetch.csv"))
-    shutil.copy(os.path.join(src, "pmc_write", "run_counter_collection.csv"), os.path.join(dst, f"{prefix}_pmc_write.csv"))
-    shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, f"{prefix}_bench.json"))
-    fetch = summarise(os.path.join(src, "pmc_fetch"), KERNEL)["FETCH_SIZE"]
-    write = summarise(os.path.join(src, "pmc_write"), KERNEL)["WRITE_SIZE"]
-    bench = json.load(open(os.path.join(src, "bench.json")))
+    copies = {"bench_ktrace/run_kernel_stats.csv": "bench_kernel_stats.csv",
+              "bench_fetch/run_counter_collection.csv": "bench_pmc_fetch.csv",
+              "bench_write/run_counter_collection.csv": "bench_pmc_write.csv",
+              "cfg_ktrace/run_kernel_stats.csv": "configs_kernel_stats.csv",
+              "cfg_fetch/run_counter_collection.csv": "configs_pmc_fetch.csv",
+              "cfg_write/run_counter_collection.csv": "configs_pmc_write.csv",
+              "configs.log": "configs.jsonl"}
+    for s, d in copies.items():
+        if os.path.exists(os.path.join(src, s)):
+            shutil.copy(os.path.join(src, s), os.path.join(dst, f"{prefix}_{d}"))
+    bench_path = os.path.join(src, "bench.json")
+    bench = last_json(bench_path if os.path.exists(bench_path) else os.path.join(src, "bench_ktrace.log"))
+    with open(os.path.join(dst, f"{prefix}_bench.json"), "w") as f:
+        f.write(json.dumps(bench) + "\n")
+
+    # per-kernel summary of the configs run
+    summary = {}
+    kst = kernel_stats(os.path.join(src, "cfg_ktrace", "run_kernel_stats.csv"))
+    for label, sub in CFG_KERNELS.items():
+        name, st = pick(kst, sub)
+        if name is None:
+            continue
+        fe = summarise(os.path.join(src, "cfg_fetch"), sub).get("FETCH_SIZE", {})
+        wr = summarise(os.path.join(src, "cfg_write"), sub).get("WRITE_SIZE", {})
+        summary[label] = {"kernel": name, **st,
+                          "fetch_bytes_per_dispatch": round(fe["fetch_bytes_x2"]) if fe else None,
+                          "write_bytes_per_dispatch": round(wr["write_bytes"]) if wr else None,
+                          "pmc_dispatches": {"FETCH_SIZE": fe.get("dispatches"), "WRITE_SIZE": wr.get("dispatches")}}
+    summary["_note"] = ("avg/min/max from rocprofv3 --kernel-trace --stats of tools/bench_configs.py --only "
+                        "varlen,shard,seal,parse --reps 10 (several workloads per kernel name are averaged "
+                        "together: the fixed validate kernel runs config 4's shard there, 3 launches of 12.5M/3 "
+                        "frames); FETCH_SIZE KiB x1024 x2 (gfx950 correction), WRITE_SIZE KiB x1024, per dispatch, "
+                        "from separate --pmc passes (--reps 3)")
+    with open(os.path.join(dst, f"{prefix}_kernels.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+
+    fetch = summarise(os.path.join(src, "bench_fetch"), BENCH_KERNEL)["FETCH_SIZE"]
+    write = summarise(os.path.join(src, "bench_write"), BENCH_KERNEL)["WRITE_SIZE"]
     out = {
         "frames": bench["config"]["frames_per_gpu"],
         "frame_len": bench["config"]["frame_len"],
@@ -35,10 +98,11 @@ def main():
         "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of `python3 bench.py "
                   "--steps 5 --warmup 2 --no-cpu-baseline` (tools/gpu_profile.sh); FETCH_SIZE KiB x1024 x2 "
                   "(gfx950 half-count correction, MI355X_MICROARCH.md HBM section), WRITE_SIZE KiB x1024; "
-                  f"raw CSVs in profiles/{prefix}_pmc_*.csv",
+                  f"raw CSVs in profiles/{prefix}_bench_pmc_*.csv",
     }
     with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
         json.dump(out, f, indent=1)
+    print(json.dumps(summary, indent=1))
     print(json.dumps(out, indent=1))
 
 

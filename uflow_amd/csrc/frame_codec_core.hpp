@@ -42,11 +42,18 @@ UFC_HD bool datagram_is_valid(const ufc_item& d) {
   return true;
 }
 
+// Where the items go: sink(k, item) for k < cap, when sink.on().  PtrSink: a plain array.
+struct PtrSink {
+  ufc_item* p;
+  UFC_HD bool on() const { return p != nullptr; }
+  UFC_HD void operator()(uint32_t k, const ufc_item& it) const { p[k] = it; }
+};
+
 // Parse the payload of a frame of `len` bytes (len >= 5) whose CRC gate passed.  Fills `info`
-// (kind, aux, f[], item_count) and, when items != nullptr, the first `cap` items.  Returns
+// (kind, aux, f[], item_count) and, when the sink is on, the first `cap` items.  Returns
 // whether Frame::read returns Some.
-template <class Rd>
-UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, ufc_item* items, uint32_t cap) {
+template <class Rd, class Sink>
+UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, const Sink& items, uint32_t cap) {
   const uint32_t plen = len - 5;  // payload = frame[1 .. len - 4]
   auto p = [&](uint32_t i) -> uint32_t { return rd(1 + i); };
   auto p32 = [&](uint32_t i) -> uint32_t { return be32(rd, 1 + i); };
@@ -124,7 +131,7 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, ufc_
         it.data_offset = 1 + pos + hs;
         it.data_len = dl;
         it.flags = datagram_is_valid(it) ? UFC_ITEM_VALID : 0;
-        if (items && k < cap) items[k] = it;
+        if (items.on() && k < cap) items(k, it);
         pos += hs + dl;
       }
       if (pos != plen) return false;  // :335-337
@@ -146,7 +153,7 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, ufc_
       if (plen - kAckPayloadHeader != UFC_ACK_GROUP_SIZE * cnt) return false;
       info.f[0] = p32(0);
       info.f[1] = p32(4);
-      if (items) {
+      if (items.on()) {
         for (uint32_t k = 0; k < cnt && k < cap; k++) {
           const uint32_t o = kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
           ufc_item it{};
@@ -154,7 +161,7 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, ufc_
           it.data_offset = p32(o + 4);  // bitfield
           it.channel_id = (uint8_t)(p(o + 8) != 0 ? 1 : 0);
           it.form = 3;
-          items[k] = it;
+          items(k, it);
         }
       }
       info.item_count = cnt;
@@ -166,9 +173,9 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, ufc_
 }
 
 // Frame::read given the CRC gate's verdict for the frame (crc_ok = len >= 5 && trailer matches).
-template <class Rd>
-UFC_HD bool read_frame(const Rd& rd, uint32_t len, bool crc_ok, ufc_frame_info& info, ufc_item* items,
-                       uint32_t cap) {
+template <class Rd, class Sink>
+UFC_HD bool read_frame_to(const Rd& rd, uint32_t len, bool crc_ok, ufc_frame_info& info, const Sink& items,
+                          uint32_t cap) {
   info.kind = len >= 1 ? (uint8_t)rd(0) : (uint8_t)0xFF;
   info.ok = 0;
   info.aux = 0;
@@ -180,6 +187,12 @@ UFC_HD bool read_frame(const Rd& rd, uint32_t len, bool crc_ok, ufc_frame_info& 
   if (!ok) info.item_count = 0;
   info.ok = ok ? 1 : 0;
   return ok;
+}
+
+template <class Rd>
+UFC_HD bool read_frame(const Rd& rd, uint32_t len, bool crc_ok, ufc_frame_info& info, ufc_item* items,
+                       uint32_t cap) {
+  return read_frame_to(rd, len, crc_ok, info, PtrSink{items}, cap);
 }
 
 }  // namespace ufc_codec
