@@ -21,7 +21,8 @@ timeout -k 10 60 $B --echo --port $port > $OUT/echo.log 2>&1 && tail -1 $OUT/ech
 for th in ${THREADS:-1 2 4}; do
   for g in cpu gpu; do
     port=$((port + 20))
-    run inline_${g}_$th --gate $g --rx-threads $th --tx-per-rx ${TXR:-2} --frames ${FRAMES:-2000000} --corrupt-every 997 --port $port
+    run inline_${g}_$th --gate $g --rx-threads $th --tx-per-rx ${TXR:-2} --batch ${BATCH:-4096} --frames ${FRAMES:-2000000} \
+      --corrupt-every 997 --port $port
   done
 done
 for g in cpu gpu; do

@@ -567,6 +567,15 @@ int run_stream_inline(const Args& a) {
               hipHostMalloc((void**)&bufs[k].valid, B, hipHostMallocDefault) != hipSuccess)
             return fail("pinned buffers");
         }
+        // size the context's per-stream staging for a full batch now (a first small batch would
+        // otherwise grow it mid-stream, and freeing device memory waits for the whole device)
+        for (int k = 0; k < 2; k++) {
+          memset(bufs[k].lens, 0, B * 4);
+          if (ufc_validate_host_slots_async(ctx, bufs[k].slots, kFrame, bufs[k].lens, B, bufs[k].crc, bufs[k].valid,
+                                            streams[k]) != UFC_OK ||
+              hipStreamSynchronize(streams[k]) != hipSuccess)
+            return fail("staging warm-up");
+        }
       } else {
         for (int k = 0; k < 2; k++) {
           bufs[k].slots = (uint8_t*)malloc(B * kFrame);
