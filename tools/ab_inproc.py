@@ -2,7 +2,9 @@
 
 Separate bench processes differ by several % from allocation to allocation, so variants are
 compared here on the same frames, interleaved, many times.  Each variant is a library path plus
-environment overrides read at launch time (e.g. UFC_LEAN_WAVES, UFC_LEAN_ABL):
+environment overrides (tuning builds, -DUFC_TUNING): each variant gets its own context, created
+with its overrides set (the kernel selection is read at ufc_ctx_create), and the overrides are
+also set around its launches (the few knobs read per launch, e.g. UFC_V8_WAVES):
 
     python tools/ab_inproc.py [--varlen] name=lib.so[,ENV=VAL...] ...
 
@@ -28,9 +30,22 @@ def load(path):
     lib.ufc_crc_batch_varlen.argtypes = [vp, vp, vp, sz, vp, vp, vp]
     lib.ufc_seal_batch_fixed.argtypes = [vp, vp, sz, sz, sz, vp, vp]
     lib.ufc_seal_batch_varlen.argtypes = [vp, vp, vp, sz, vp, vp]
+    return lib
+
+
+def make_ctx(lib, env):
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     ctx = ctypes.c_void_p()
-    assert lib.ufc_ctx_create(ctypes.byref(ctx), 0) == 0, path
-    return lib, ctx
+    try:
+        assert lib.ufc_ctx_create(ctypes.byref(ctx), 0) == 0
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+    return ctx
 
 
 def main():
@@ -47,7 +62,8 @@ def main():
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
-    libs = {path: load(path) for _, path, _ in variants}
+    loaded = {path: load(path) for _, path, _ in variants}
+    libs = {name: (loaded[path], make_ctx(loaded[path], env)) for name, path, env in variants}
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED0001)
     crc = valid = offs = None
@@ -59,13 +75,13 @@ def main():
         o[1:] = np.cumsum(lens)
         offs = torch.from_numpy(o.view(np.int64)).to(dev)
         frames = torch.randint(0, 256, (int(o[-1]),), dtype=torch.uint8, device=dev, generator=g)
-        lib0, ctx0 = libs[variants[0][1]]
+        lib0, ctx0 = libs[variants[0][0]]
         assert lib0.ufc_seal_batch_varlen(ctx0, frames.data_ptr(), offs.data_ptr(), n, None, sp) == 0
         nbytes = int(o[-1])
     else:
         n, L = int(os.environ.get("FX_N", 1_000_000)), int(os.environ.get("FX_LEN", 1500))
         frames = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=g)
-        lib0, ctx0 = libs[variants[0][1]]
+        lib0, ctx0 = libs[variants[0][0]]
         assert lib0.ufc_seal_batch_fixed(ctx0, frames.data_ptr(), L, L, n, None, sp) == 0
         nbytes = n * L
     idx = torch.arange(0, n, 1000, device=dev)
@@ -93,7 +109,7 @@ def main():
         for name, path, env in variants:
             saved = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
-            lib, ctx = libs[path]
+            lib, ctx = libs[name]
             launch(lib, ctx)
             evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
             for e0, e1 in evs:
