@@ -82,6 +82,29 @@ __device__ __forceinline__ uint32_t group_lin8(const Lane8& L, const Chains& c) 
   return v;
 }
 
+// Front-fix table in LDS: for p = 0..20 bytes of a 16-byte piece before its frame, the mask M of
+// the frame's bytes and the bytes Gs of G placed before them, so that front_fix(x, p, G) =
+// (x & M) | Gs (p <= 0: nothing to fix, p >= 20: all zero).  32 bytes per entry, in the unused
+// upper halves (columns 32..63) of the 32-slot nibble image's first rows.
+constexpr int kFixEntries = 21;
+__device__ __forceinline__ uint32_t fixtab_addr(uint32_t i) { return (i >> 2) * 256u + 128u + (i & 3u) * 32u; }
+
+__device__ __forceinline__ void fixtab_store(char* lds, uint32_t G) {  // threads 0..20, after the staging
+  const uint32_t t = threadIdx.x;
+  if (t < (uint32_t)kFixEntries) {
+    const uint4 m = front_fix(make_uint4(~0u, ~0u, ~0u, ~0u), (int)t, G), g = front_fix(make_uint4(0u, 0u, 0u, 0u), (int)t, G);
+    *(uint4*)(lds + fixtab_addr(t)) = make_uint4(m.x & ~g.x, m.y & ~g.y, m.z & ~g.z, m.w & ~g.w);
+    *(uint4*)(lds + fixtab_addr(t) + 16) = g;
+  }
+}
+
+__device__ __forceinline__ uint4 fix_piece(const char* lds, uint4 x, int p) {
+  const uint32_t i = (uint32_t)min(max(p, 0), kFixEntries - 1);
+  const uint4 m = *(const uint4*)(lds + fixtab_addr(i)), g = *(const uint4*)(lds + fixtab_addr(i) + 16);
+  return make_uint4(__builtin_amdgcn_bitop3_b32(x.x, m.x, g.x, 0xEA), __builtin_amdgcn_bitop3_b32(x.y, m.y, g.y, 0xEA),
+                    __builtin_amdgcn_bitop3_b32(x.z, m.z, g.z, 0xEA), __builtin_amdgcn_bitop3_b32(x.w, m.w, g.w, 0xEA));
+}
+
 __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
   c.v0 = chain_step(L.lds, c.v0, L.K, x.x);
   c.v1 = chain_step(L.lds, c.v1, L.K, x.y);
@@ -101,8 +124,8 @@ __device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, u
     x1.w = (L.col == 7u) ? 0u : x1.w;
   }
   if (j == 0) {
-    const uint4 f0 = front_fix(x0, (int)pad - (int)(16u * L.col), L.G);
-    x1 = front_fix(x1, (int)pad - 128 - (int)(16u * L.col), L.G);
+    const uint4 f0 = fix_piece(L.lds, x0, (int)pad - (int)(16u * L.col));
+    x1 = fix_piece(L.lds, x1, (int)pad - 128 - (int)(16u * L.col));
     c.v0 = f0.x;
     c.v1 = f0.y;
     c.v2 = f0.z;
@@ -337,6 +360,10 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   }
   O[DEPTH - 1] = Rq[DEPTH - 1];
   stage_store<WAVES * 64>(sr, lds);
+  fixtab_store(lds, p.G);  // (then an LDS-only barrier, as in stage_store: the prefetches stay in flight)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 
   // One step: geometry + loads of set S + DEPTH - 1 (record loaded DEPTH steps ago), the record of
   // set S + 2 DEPTH - 1, then compute set S.
