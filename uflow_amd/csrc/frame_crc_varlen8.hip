@@ -232,13 +232,16 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   // and blocks past it are out of range.
   auto load_set = [&](uint32_t voff0, uint32_t geo, Buf8<JM>& b) {
     const uint32_t J = v8_J(geo), pad = v8_pad(geo), dl = (geo >> 13) & 3u;
+    // one select per block (the constant part of each offset goes into the instruction's offset
+    // field; an out-of-range base stays out of range with it)
 #pragma unroll
     for (int j = 0; j < JM; j++) {
+      const uint32_t base = ((uint32_t)j < J) ? voff0 : kV8Oob;
 #pragma unroll
       for (int h = 0; h < 2; h++) {
-        uint32_t vo = ((uint32_t)j < J) ? voff0 + 256u * j + 128u * h : kV8Oob;
+        uint32_t vo = base;
         if (j == 0) vo = (128u * h + 16u * L.col + 16u + dl <= pad) ? kV8Oob : vo;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8Aux);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, kV8Aux);
         b.x[2 * j + h] = make_uint4(v.x, v.y, v.z, v.w);
       }
     }
