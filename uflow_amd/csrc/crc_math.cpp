@@ -133,11 +133,45 @@ void build_nibble_image(uint32_t out[8192]) {
   }
 }
 
+// The inverse of A^nbytes (GF(2) Gauss-Jordan on the 32 columns), applied to v.
+uint32_t retreat(uint32_t v, uint64_t nbytes) {
+  uint32_t cols[32];
+  for (int i = 0; i < 32; i++) cols[i] = advance(1u << i, nbytes);
+  // rows of [M | I]: row r = bits r of the columns (M part) and e_r (identity part)
+  uint64_t rows[32];
+  for (int r = 0; r < 32; r++) {
+    uint64_t row = (uint64_t)1 << (32 + r);
+    for (int c = 0; c < 32; c++) row |= (uint64_t)((cols[c] >> r) & 1u) << c;
+    rows[r] = row;
+  }
+  for (int c = 0; c < 32; c++) {
+    int piv = -1;
+    for (int r = c; r < 32; r++)
+      if ((rows[r] >> c) & 1u) { piv = r; break; }
+    if (piv < 0) return 0;  // (A is invertible: not reached)
+    const uint64_t t = rows[c]; rows[c] = rows[piv]; rows[piv] = t;
+    for (int r = 0; r < 32; r++)
+      if (r != c && ((rows[r] >> c) & 1u)) rows[r] ^= rows[c];
+  }
+  // rows[r] = [e_r | row r of M^-1]: x = M^-1 v, x_r = parity(rowinv_r & v)
+  uint32_t x = 0;
+  for (int r = 0; r < 32; r++) x |= (uint32_t)(__builtin_popcount((uint32_t)(rows[r] >> 32) & v) & 1) << r;
+  return x;
+}
+
 void build_nibble_image32(uint32_t out[8192]) {
   for (int c = 0; c < 64; c++)
     for (int k = 0; k < 8; k++)
-      for (int e = 0; e < 16; e++)
-        out[(k * 16 + e) * 64 + c] = c < 32 ? advance((uint32_t)e << (4 * k), (uint64_t)4 * (31 - c)) : 0u;
+      for (int e = 0; e < 16; e++) {
+        uint32_t v = 0;
+        if (c < 32) {
+          v = advance((uint32_t)e << (4 * k), (uint64_t)4 * (31 - c));
+        } else if (c >= 40 && c < 52) {  // A^-8t for t = 1..3, one copy per 8-lane group mod 4
+          const int t = (c - 40) % 3 + 1;
+          v = retreat((uint32_t)e << (4 * k), (uint64_t)t);
+        }
+        out[(k * 16 + e) * 64 + c] = v;
+      }
 }
 
 }  // namespace ufc

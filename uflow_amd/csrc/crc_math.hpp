@@ -37,9 +37,12 @@ uint32_t host_extend(uint32_t initial_crc, const uint8_t* data, size_t len);
 // Device table images (layouts documented in frame_crc.hip):
 //   chain[k*256 + e] = A^nbytes(e << 8k)                    k = 0..3, e = 0..255   (1024 words)
 //   nib[(k*16 + e)*64 + c] = A^(4(63 - s))(e << 4k),  s = ((c & 31) << 1) | (c >> 5)  (8192 words)
-//   nib32[(k*16 + e)*64 + c] = A^(4(31 - c))(e << 4k) for c < 32, 0 above (8-lane frames, 32 slots)
+//   nib32[(k*16 + e)*64 + c] = A^(4(31 - c))(e << 4k) for c < 32 (8-lane frames, 32 slots);
+//     columns 40 + 3 g + (t - 1), g = 0..3, t = 1..3: A^-t(e << 4k) (bytes past a frame's end); 0 else
 void build_chain_table(uint32_t out[1024], uint64_t nbytes);
 void build_nibble_image(uint32_t out[8192]);
 void build_nibble_image32(uint32_t out[8192]);
+// A^-nbytes(v): the register before nbytes zero bytes that leave it at v.
+uint32_t retreat(uint32_t v, uint64_t nbytes);
 
 }  // namespace ufc

@@ -18,10 +18,13 @@
 //   * Sets come from run-sorted records (sort_runs, frame_crc_varlen.hip): a run of 64 frames is
 //     ordered by block count J, so a set's 8 frames mostly share J (one uniform block loop, no
 //     frozen chains); a set mixing block counts freezes the chains of its shorter frames.
-//   * Loads are default-policy raw buffer loads from one resource per wave (4-byte-aligned, the
-//     frame's window rebuilt with one v_perm per word; the lines a frame shares with its
-//     neighbours, which sort into other sets, stay in L2 for them).  Lanes wholly before their
-//     frame and blocks past it load nothing (out-of-range offsets).
+//   * Windows end at the frame's end rounded up to 4 bytes, so every load is 4-byte aligned and
+//     needs no realignment: the t = 0..3 bytes past the frame are zeroed with the trailer, which
+//     multiplies the linear CRC by A^t, undone at the finish with one nibble-table product
+//     (A^-t, 8 lookups per frame instead of one v_perm per word and 4 DPP moves per block).
+//   * Loads are default-policy raw buffer loads from one resource per wave (the lines a frame
+//     shares with its neighbours, which sort into other sets, stay in L2 for them).  Lanes wholly
+//     before their frame and blocks past it load nothing (out-of-range offsets).
 //   * Results of a run (8 sets x 8 frames) collect in one register pair per lane and leave with
 //     hidden stores once per run.  Sets with a frame the fast path cannot take (shorter than 4 B,
 //     longer than 6 blocks, at the batch edges, past its end) run byte-wise, in the same loop.
@@ -37,11 +40,11 @@ constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no mem
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
 constexpr int kV8Aux = 0;                  // default cache policy (shared boundary lines)
 
-// Per-lane geometry of a set (one VGPR): pad [0,9), J [9,12), len >= 5 [12], dl [13,15), frame
-// index in its run [16,22), past the batch end [22].
+// Per-lane geometry of a set (one VGPR): pad [0,9), J [9,12), len >= 5 [12], t [13,15) (window
+// bytes past the frame), frame index in its run [16,22), past the batch end [22].
 __device__ __forceinline__ uint32_t v8_pad(uint32_t g) { return g & 511u; }
 __device__ __forceinline__ uint32_t v8_J(uint32_t g) { return (g >> 9) & 7u; }
-__device__ __forceinline__ uint32_t v8_sel(uint32_t g) { return 0x03020100u + (4u - ((g >> 13) & 3u)) * 0x01010101u; }
+__device__ __forceinline__ uint32_t v8_t(uint32_t g) { return (g >> 13) & 3u; }
 __device__ __forceinline__ uint32_t v8_orig(uint32_t g) { return (g >> 16) & 63u; }
 
 struct Lane8 {
@@ -85,9 +88,9 @@ __device__ __forceinline__ uint32_t group_lin8(const Lane8& L, const Chains& c) 
 // Front-fix table in LDS: for p = 0..20 bytes of a 16-byte piece before its frame, the mask M of
 // the frame's bytes and the bytes Gs of G placed before them, so that front_fix(x, p, G) =
 // (x & M) | Gs (p <= 0: nothing to fix, p >= 20: all zero).  32 bytes per entry, in the unused
-// upper halves (columns 32..63) of the 32-slot nibble image's first rows.
+// columns 32..39 of the 32-slot nibble image's rows 0..20 (columns 40..51 hold the A^-t tables).
 constexpr int kFixEntries = 21;
-__device__ __forceinline__ uint32_t fixtab_addr(uint32_t i) { return (i >> 2) * 256u + 128u + (i & 3u) * 32u; }
+__device__ __forceinline__ uint32_t fixtab_addr(uint32_t i) { return i * 256u + 128u; }
 
 __device__ __forceinline__ void fixtab_store(char* lds, uint32_t G) {  // threads 0..20, after the staging
   const uint32_t t = threadIdx.x;
@@ -114,14 +117,17 @@ __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
 
 // One 256-byte block j of a frame (pieces x0 at 16 col, x1 at 128 + 16 col, window-aligned):
 // front fix of block 0 (and of block 1's first word when G straddles into it), trailer capture on
-// the frame's last block (lane 7's last word of piece 1), two A^128 steps.  FREEZE: chains stop
-// after the frame's own J blocks.
+// the frame's last block (in lane 7, the 4 bytes before the window's last t), two A^128 steps.
+// FREEZE: chains stop after the frame's own J blocks.
 template <bool FREEZE>
-__device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, uint32_t pad, bool g1, bool last_any,
-                                       uint4 x0, uint4 x1, Chains& c) {
+__device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, uint32_t pad, uint32_t t, bool g1,
+                                       bool last_any, uint4 x0, uint4 x1, Chains& c) {
   if (FREEZE ? (j + 1 == J) : last_any) {
-    c.tr = x1.w;
-    x1.w = (L.col == 7u) ? 0u : x1.w;
+    c.tr = t ? __builtin_amdgcn_alignbyte(x1.w, x1.z, 4u - t) : x1.w;
+    if (L.col == 7u) {  // the trailer and the bytes past the frame are CRC'd as zeros
+      x1.z &= 0xFFFFFFFFu >> (8u * t);
+      x1.w = 0u;
+    }
   }
   if (j == 0) {
     const uint4 f0 = fix_piece(L.lds, x0, (int)pad - (int)(16u * L.col));
@@ -205,11 +211,11 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const uint32_t len = min(r.z, 0x40000000u);  // (longer: J > 6, the byte path)
     const bool dead = (r.w >> 31) != 0;
-    const uint32_t J = (len + 4u + 255u) >> 8;
-    const uint32_t pad = (J * 256u - len) & 511u;
+    const uint32_t t = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a + len)) & 3u;  // end up to 4 B
+    const uint32_t J = (len + t + 4u + 255u) >> 8;
+    const uint32_t pad = (J * 256u - len - t) & 511u;
     const uint64_t rel64 = a - b0;  // (a >= b0 for CSR; pairs: b0 = 0)
-    const uint32_t wrel = (uint32_t)rel64 + kV8Bias - pad;  // window start
-    const uint32_t dl = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - pad)) & 3u;
+    const uint32_t wrel = (uint32_t)rel64 + kV8Bias - pad;  // window start (4-byte aligned)
     const bool bad = dead || len < 4u || J > (uint32_t)JM || a < (uint64_t)pad || a + len + 3 > buf_end ||
                      rel64 >= (uint64_t)kV8Limit;
     m.slow = __builtin_amdgcn_ballot_w64(bad) != 0;
@@ -224,14 +230,14 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     m.mixed = jmin != jmax;
     m.g1 = __builtin_amdgcn_ballot_w64(pad > 256u) != 0;
     const bool live = q < q_end && !m.slow;
-    voff0 = live ? wrel + dl + 16u * L.col : kV8Oob;
-    return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (dl << 13) | ((r.w & 63u) << 16) |
+    voff0 = live ? wrel + 16u * L.col : kV8Oob;
+    return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | ((r.w & 63u) << 16) |
            ((dead ? 1u : 0u) << 22);
   };
   // The set's loads: block j's pieces at voff0 + 256 j (+ 128); pieces wholly before the frame
   // and blocks past it are out of range.
   auto load_set = [&](uint32_t voff0, uint32_t geo, Buf8<JM>& b) {
-    const uint32_t J = v8_J(geo), pad = v8_pad(geo), dl = (geo >> 13) & 3u;
+    const uint32_t J = v8_J(geo), pad = v8_pad(geo);
     // one select per block (the constant part of each offset goes into the instruction's offset
     // field; an out-of-range base stays out of range with it)
 #pragma unroll
@@ -240,7 +246,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         uint32_t vo = base;
-        if (j == 0) vo = (128u * h + 16u * L.col + 16u + dl <= pad) ? kV8Oob : vo;
+        if (j == 0) vo = (128u * h + 16u * L.col + 16u <= pad) ? kV8Oob : vo;
         const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, kV8Aux);
         b.x[2 * j + h] = make_uint4(v.x, v.y, v.z, v.w);
       }
@@ -260,41 +266,40 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_qv >> 31);
     }
   };
+  // A^-t of every group's lin (t from the geometry; the 32-slot image's columns 40 + 3 (g & 3) +
+  // t - 1 hold the nibble tables, one copy per group of a half-wave: no bank conflicts).
+  auto unshift = [&](uint32_t lin, uint32_t geo) -> uint32_t {
+    const uint32_t t = v8_t(geo);
+    if (__builtin_amdgcn_ballot_w64(t != 0) == 0) return lin;
+    const uint32_t col = 40u + 3u * (L.grp & 3u) + (t ? t - 1u : 0u);
+    const uint32_t r = nib_mul<0>(L.lds, lin, col * 4u);
+    return t ? r : lin;
+  };
   // The result of a set (crc in every lane of a group; trailer word in its lane 7).
   auto finish = [&](uint32_t q, uint32_t geo, const Chains& c, uint32_t voff0) {
-    const uint32_t crc = ~group_lin8(L, c);
+    const uint32_t crc = ~unshift(group_lin8(L, c), geo);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
     const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     if (SEAL && L.col >= 4u && !((geo >> 22) & 1u)) {  // BE32 trailer: lane 4 + k writes byte k
-      const uint32_t k = L.col - 4u, dl = (geo >> 13) & 3u;
-      st_u8_hidden((uint8_t*)p.wbytes + (base - p.bytes) + (voff0 - dl - 16u * L.col + 256u * v8_J(geo) - 4u + k),
+      const uint32_t k = L.col - 4u;
+      st_u8_hidden((uint8_t*)p.wbytes + (base - p.bytes) + (voff0 - 16u * L.col + 256u * v8_J(geo) - v8_t(geo) - 4u + k),
                    crc >> (24 - 8 * k));
     }
     record(q & 7u, crc, v8_orig(geo) | (ok << 31) | (((geo >> 22) & 1u) << 30));
     if ((q & 7u) == 7u) store_run(q >> 3);
   };
 
-  // Fast set: Jset blocks (uniform), realigned pieces.
+  // Fast set: Jset blocks (uniform), the loaded pieces as they are.
   auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf8<JM>& b, uint32_t voff0) {
-    const uint32_t J = v8_J(geo), pad = v8_pad(geo), sel = v8_sel(geo);
-    uint32_t rp = 0;  // lane 7's last loaded word of the previous block's piece 1 (for lane 0)
+    const uint32_t J = v8_J(geo), pad = v8_pad(geo), t = v8_t(geo);
     Chains c{0u, 0u, 0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < JM; j++) {
       if ((uint32_t)j < m.Jset) {
-        const uint4 w0 = b.x[2 * j], w1 = b.x[2 * j + 1];
-        const uint32_t r1a = (uint32_t)__builtin_amdgcn_mov_dpp((int)w0.w, 0x121, 0xF, 0xF, false);  // row_ror:1
-        const uint32_t r1b = (uint32_t)__builtin_amdgcn_mov_dpp((int)w1.w, 0x121, 0xF, 0xF, false);
-        const uint32_t r9a = (uint32_t)__builtin_amdgcn_mov_dpp((int)w0.w, 0x129, 0xF, 0xF, false);  // row_ror:9
-        const uint32_t r9b = (uint32_t)__builtin_amdgcn_mov_dpp((int)w1.w, 0x129, 0xF, 0xF, false);
-        const uint32_t pa = (L.col == 0u) ? rp : r1a, pb = (L.col == 0u) ? r9a : r1b;
-        rp = r9b;
-        const uint4 x0 = make_uint4(perm(w0.x, pa, sel), perm(w0.y, w0.x, sel), perm(w0.z, w0.y, sel), perm(w0.w, w0.z, sel));
-        const uint4 x1 = make_uint4(perm(w1.x, pb, sel), perm(w1.y, w1.x, sel), perm(w1.z, w1.y, sel), perm(w1.w, w1.z, sel));
         if (m.mixed)
-          block8<true>(L, (uint32_t)j, J, pad, m.g1, false, x0, x1, c);
+          block8<true>(L, (uint32_t)j, J, pad, t, m.g1, false, b.x[2 * j], b.x[2 * j + 1], c);
         else
-          block8<false>(L, (uint32_t)j, J, pad, m.g1, (uint32_t)j + 1 == m.Jset, x0, x1, c);
+          block8<false>(L, (uint32_t)j, J, pad, t, m.g1, (uint32_t)j + 1 == m.Jset, b.x[2 * j], b.x[2 * j + 1], c);
       }
     }
     finish(q, geo, c, voff0);
@@ -326,7 +331,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       const int o0 = 256 * (int)jb + 16 * (int)L.col - d.pad;
       const uint4 x0 = make_uint4(word(o0), word(o0 + 4), word(o0 + 8), word(o0 + 12));
       const uint4 x1 = make_uint4(word(o0 + 128), word(o0 + 132), word(o0 + 136), word(o0 + 140));
-      block8<true>(L, j, (uint32_t)d.J, (uint32_t)d.pad, true, false, x0, x1, c);
+      block8<true>(L, j, (uint32_t)d.J, (uint32_t)d.pad, 0u, true, false, x0, x1, c);
     }
     const uint32_t geo = ((d.len >= 5u ? 1u : 0u) << 12) | ((r.w & 63u) << 16) | ((dead ? 1u : 0u) << 22);
     const uint32_t crc = ~group_lin8(L, c);
