@@ -316,21 +316,35 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 #pragma unroll
     for (int g = 0; g < 8; g++) nb = max(nb, (uint32_t)__builtin_amdgcn_readlane(d.J, 8 * g));
     Chains c{0u, 0u, 0u, 0u, 0u};
-    auto word = [&](int o) -> uint32_t {  // frame bytes [o, o + 4), zeros outside the frame
-      uint32_t v = 0;
-#pragma unroll 1
-      for (int k = 0; k < 4; k++) {
-        const int ob = o + k;
-        if (ob >= 0 && ob < (int)d.len) v |= (uint32_t)*as_global<g_u8>(p.bytes + d.start + (uint64_t)ob) << (8 * k);
+    // Frame bytes [o, o + 16), zeros outside the frame: the five 4-byte-aligned words over them,
+    // each loaded only if it holds a frame byte (an aligned word holding a valid byte never
+    // crosses a page), realigned and masked to the frame.  All loads independent.
+    const uintptr_t f0 = (uintptr_t)p.bytes + (uintptr_t)d.start, f1 = f0 + d.len;
+    auto piece = [&](int o) -> uint4 {
+      const uintptr_t P = f0 + (intptr_t)o, A = P & ~(uintptr_t)3;
+      const uint32_t sh = (uint32_t)(P & 3u);
+      uint32_t w[5];
+#pragma unroll
+      for (int k = 0; k < 5; k++) {
+        const uintptr_t ak = A + 4 * k;
+        w[k] = (ak < f1 && ak + 4 > f0) ? *as_global<g_u32>((const uint32_t*)ak) : 0u;
       }
-      return v;
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const int ob = o + 4 * i;  // frame offset of the word's first byte
+        const uint32_t lo = (uint32_t)min(max(-ob, 0), 4), hi = (uint32_t)min(max((int)d.len - ob, 0), 4);
+        const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u), mlo = lo >= 4u ? 0u : (~0u << (8u * lo));
+        x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh) & mhi & mlo;
+      }
+      return make_uint4(x[0], x[1], x[2], x[3]);
     };
 #pragma unroll 1
     for (uint32_t j = 0; j < nb; j++) {
       const uint32_t jb = min(j, (uint32_t)d.J - 1u);
       const int o0 = 256 * (int)jb + 16 * (int)L.col - d.pad;
-      const uint4 x0 = make_uint4(word(o0), word(o0 + 4), word(o0 + 8), word(o0 + 12));
-      const uint4 x1 = make_uint4(word(o0 + 128), word(o0 + 132), word(o0 + 136), word(o0 + 140));
+      const uint4 x0 = piece(o0);
+      const uint4 x1 = piece(o0 + 128);
       block8<true>(L, j, (uint32_t)d.J, (uint32_t)d.pad, 0u, true, false, x0, x1, c);
     }
     const uint32_t geo = ((d.len >= 5u ? 1u : 0u) << 12) | ((r.w & 63u) << 16) | ((dead ? 1u : 0u) << 22);
