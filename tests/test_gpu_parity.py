@@ -323,6 +323,40 @@ def test_pairs_gapped_layout(engine):
     assert np.array_equal(crc.cpu().numpy().view(np.uint32), np.array([c for _, c in ref], np.uint32))
 
 
+def test_pairs_beyond_2gb(engine):
+    """(start, end) pairs over a 2.2 GB buffer: frames near its start and past 2^31, in random
+    order (sets mixing both regions take the kernel's byte path, the others the fast path)."""
+    rng = np.random.default_rng(63)
+    regions = (3, (1 << 31) + 5_000_003)
+    size = regions[1] + 9_000_000
+    buf = torch.zeros(size, dtype=torch.uint8, device=DEV)
+    pairs, ref = [], []
+    for base in regions:
+        lens = rng.integers(0, 1600, size=5_000)
+        gaps = rng.integers(0, 30, size=lens.size)
+        starts = np.cumsum(np.concatenate([[0], (lens + gaps)[:-1]]))
+        host = _rand_bytes(rng, int(starts[-1] + lens[-1]) + 8)
+        for i, (s, l) in enumerate(zip(starts, lens)):
+            if l >= 4:
+                fr = bytearray(host[s:s + l].tobytes())
+                if i % 37:
+                    oracle.frame_seal(fr)
+                host[s:s + l] = np.frombuffer(bytes(fr), np.uint8)
+            ref.append(oracle.frame_validate(host[s:s + l].tobytes()))
+            pairs.append((base + s, base + s + l))
+        buf[base:base + host.size] = torch.from_numpy(host).to(DEV)
+    # half of each region's frames in order (fast sets), the rest of both regions shuffled together
+    rest = np.concatenate([np.arange(2_500, 5_000), 7_500 + np.arange(2_500)])
+    order = np.concatenate([np.arange(2_500), 5_000 + np.arange(2_500), rng.permutation(rest)])
+    pairs = np.array(pairs, np.int64)[order]
+    ref = [ref[i] for i in order]
+    crc, valid = engine.crc_pairs(buf, torch.from_numpy(pairs).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(valid.cpu().numpy(), np.array([int(v) for v, _ in ref], np.uint8))
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), np.array([c for _, c in ref], np.uint32))
+    del buf
+
+
 def test_host_slots(engine):
     """The receive loop's recvmmsg layout: fixed 1472-B slots with per-datagram lengths."""
     rng = np.random.default_rng(62)

@@ -204,3 +204,21 @@ def test_seal_host_entry_points_reject_null_buffers():
     # no context: invalid argument (never a crash); zero frames: nothing to do
     assert l.ufc_seal_host_slots(null, None, 1472, None, 4, scratch) == _native.UFC_ERR_INVALID_ARG
     assert l.ufc_seal_host_varlen(null, None, None, 4, scratch) == _native.UFC_ERR_INVALID_ARG
+
+
+def test_gpu_box_receives_what_gpu_runs_load():
+    """.gpurunignore keeps the built library and the PMC summary bench.py reads (roofline.traffic)
+    in the snapshot sent to the GPU box (tar-style patterns: a leading ./ anchors at the top)."""
+    import fnmatch
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(repo, ".gpurunignore")) as f:
+        pats = [l.strip() for l in f if l.strip() and not l.startswith("#")]
+    for path in ("profiles/pmc_traffic.json", "uflow_amd/libuflowcrc.so", "oracle/liboracle.so", "bench.py",
+                 "tools/loopback/ufc_loopback", "tests/golden/kat.json"):
+        for p in pats:
+            anchored = p.startswith("./")
+            pat = p[2:] if anchored else p
+            hit = fnmatch.fnmatch(path, pat) or (not anchored and fnmatch.fnmatch(os.path.basename(path), pat)) \
+                or path.startswith(pat.rstrip("/") + "/")
+            assert not hit, f"{p} in .gpurunignore drops {path}"

@@ -35,7 +35,7 @@ namespace ufc_dev {
 namespace {
 
 constexpr int kV8Blocks = 6;               // fast path: frames of 4..1532 B
-constexpr uint32_t kV8Bias = 1024;         // lane offsets: relative to the wave's base - bias
+constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the set's base - bias
 constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
 constexpr int kV8Aux = 0;                  // default cache policy (shared boundary lines)
@@ -185,39 +185,40 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   const uint32_t nruns = (uint32_t)((nfr + kRunFrames - 1) / kRunFrames);
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t W = gridDim.x * WAVES, w = blockIdx.x * WAVES + wid;
+  // This wave's sets: a contiguous range of runs (8 sets per run of 64 frames); k = 0 .. nk - 1
+  // is set setq(k) of the batch.  (Runs w, w + W, ... instead, every wave sweeping the batch
+  // together, measured the same.)
   const uint32_t R0 = (uint32_t)((uint64_t)nruns * w / W), R1 = (uint32_t)((uint64_t)nruns * (w + 1) / W);
-  const uint32_t q_lo = R0 * 8u, q_end = R1 * 8u;  // this wave's sets (8 per run)
+  const uint32_t nk = (R1 - R0) * 8u;
+  auto setq = [&](uint32_t k) -> uint32_t { return R0 * 8u + k; };
   const uint4* rec = (const uint4*)p.offsets;
-  // The wave's base: its first frame's start (CSR offsets grow), or the buffer itself (pairs).
-  uint64_t b0 = 0;
-  if (!PAIRS && R0 < R1) {
-    const uint64_t v = *as_global<g_u64>(p.offsets_csr + (uint64_t)R0 * kRunFrames);
-    b0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
-         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
-    b0 &= ~3ull;
-  }
-  const uint8_t* base = p.bytes + b0 - kV8Bias;
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)0x7FFFFFF0, 0x00020000);
   const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets_csr + nfr);
 
-  // This group's record of set q (the same 16 bytes in the group's 8 lanes).
-  auto load_rec = [&](uint32_t q) -> uint4 {
-    const uint32_t qc = q_end > q_lo ? min(q, q_end - 1) : 0u;  // (a wave without runs reads set 0)
+  // This group's record of the wave's set k (the same 16 bytes in the group's 8 lanes).
+  auto load_rec = [&](uint32_t k) -> uint4 {
+    const uint32_t qc = nk ? setq(min(k, nk - 1u)) : 0u;  // (a wave without runs reads set 0)
     const u32x4 r = *as_global<g_u32x4>((const uint32_t*)(rec + (uint64_t)qc * 8 + L.grp));
     return make_uint4(r.x, r.y, r.z, r.w);
   };
-  // Geometry of set q from its record: packed per-lane geometry, block-0 piece-0 offset, meta.
-  auto geometry = [&](uint32_t q, uint4 r, uint32_t& voff0, Set8Meta& m) -> uint32_t {
+  // Geometry of the wave's set k from its record: packed per-lane geometry, block-0 piece-0
+  // offset, meta, and the set's base (buffer offset of its loads' resource, minus a bias): its
+  // group-0 frame's start (CSR: the fast frames of a run lie within 64 x 1.5 KB of each other),
+  // or the buffer itself for pairs over less than 2 GB (pairs may come in any order).
+  const bool flat = PAIRS && p.frame_len < (1ull << 31) - (1ull << 20);
+  auto geometry = [&](uint32_t k, uint4 r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const uint32_t len = min(r.z, 0x40000000u);  // (longer: J > 6, the byte path)
     const bool dead = (r.w >> 31) != 0;
     const uint32_t t = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a + len)) & 3u;  // end up to 4 B
     const uint32_t J = (len + t + 4u + 255u) >> 8;
     const uint32_t pad = (J * 256u - len - t) & 511u;
-    const uint64_t rel64 = a - b0;  // (a >= b0 for CSR; pairs: b0 = 0)
-    const uint32_t wrel = (uint32_t)rel64 + kV8Bias - pad;  // window start (4-byte aligned)
+    sb = flat ? 0u : (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.x) |
+                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.y) << 32)) & ~3ull);
+    sb -= kV8Bias;
+    const uint64_t rel64 = a - sb;
+    const uint32_t wrel = (uint32_t)rel64 - pad;  // window start (4-byte aligned)
     const bool bad = dead || len < 4u || J > (uint32_t)JM || a < (uint64_t)pad || a + len + 3 > buf_end ||
-                     rel64 >= (uint64_t)kV8Limit;
+                     rel64 >= (uint64_t)kV8Limit || rel64 < 512u;
     m.slow = __builtin_amdgcn_ballot_w64(bad) != 0;
     uint32_t jmax = 0, jmin = 7;
 #pragma unroll
@@ -229,15 +230,16 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     m.Jset = min(jmax, (uint32_t)JM);
     m.mixed = jmin != jmax;
     m.g1 = __builtin_amdgcn_ballot_w64(pad > 256u) != 0;
-    const bool live = q < q_end && !m.slow;
+    const bool live = k < nk && !m.slow;
     voff0 = live ? wrel + 16u * L.col : kV8Oob;
     return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | ((r.w & 63u) << 16) |
            ((dead ? 1u : 0u) << 22);
   };
   // The set's loads: block j's pieces at voff0 + 256 j (+ 128); pieces wholly before the frame
   // and blocks past it are out of range.
-  auto load_set = [&](uint32_t voff0, uint32_t geo, Buf8<JM>& b) {
+  auto load_set = [&](uint32_t voff0, uint32_t geo, uint64_t sb, Buf8<JM>& b) {
     const uint32_t J = v8_J(geo), pad = v8_pad(geo);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
     // one select per block (the constant part of each offset goes into the instruction's offset
     // field; an out-of-range base stays out of range with it)
 #pragma unroll
@@ -276,13 +278,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     return t ? r : lin;
   };
   // The result of a set (crc in every lane of a group; trailer word in its lane 7).
-  auto finish = [&](uint32_t q, uint32_t geo, const Chains& c, uint32_t voff0) {
+  auto finish = [&](uint32_t q, uint32_t geo, const Chains& c, uint32_t voff0, uint64_t sb) {
     const uint32_t crc = ~unshift(group_lin8(L, c), geo);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
     const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     if (SEAL && L.col >= 4u && !((geo >> 22) & 1u)) {  // BE32 trailer: lane 4 + k writes byte k
       const uint32_t k = L.col - 4u;
-      st_u8_hidden((uint8_t*)p.wbytes + (base - p.bytes) + (voff0 - 16u * L.col + 256u * v8_J(geo) - v8_t(geo) - 4u + k),
+      st_u8_hidden((uint8_t*)p.wbytes + sb + (voff0 - 16u * L.col + 256u * v8_J(geo) - v8_t(geo) - 4u + k),
                    crc >> (24 - 8 * k));
     }
     record(q & 7u, crc, v8_orig(geo) | (ok << 31) | (((geo >> 22) & 1u) << 30));
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   };
 
   // Fast set: Jset blocks (uniform), the loaded pieces as they are.
-  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf8<JM>& b, uint32_t voff0) {
+  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf8<JM>& b, uint32_t voff0, uint64_t sb) {
     const uint32_t J = v8_J(geo), pad = v8_pad(geo), t = v8_t(geo);
     Chains c{0u, 0u, 0u, 0u, 0u};
 #pragma unroll
@@ -302,12 +304,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
           block8<false>(L, (uint32_t)j, J, pad, t, m.g1, (uint32_t)j + 1 == m.Jset, b.x[2 * j], b.x[2 * j + 1], c);
       }
     }
-    finish(q, geo, c, voff0);
+    finish(q, geo, c, voff0, sb);
   };
 
   // Byte path of set q: any lengths, loads restricted to each frame; the same result handling.
-  auto slow_set = [&](uint32_t q) {
-    const uint4 r = load_rec(q);
+  auto slow_set = [&](uint32_t k) {
+    const uint4 r = load_rec(k);
+    const uint32_t q = setq(k);
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const bool dead = (r.w >> 31) != 0;
     const uint32_t len = dead ? 0u : r.z;
@@ -368,16 +371,17 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   Buf8<JM> B[DEPTH];
   uint4 O[DEPTH];
   uint32_t GE[DEPTH], VO[DEPTH];
+  uint64_t SB[DEPTH];
   Set8Meta M[DEPTH];
-  uint32_t S = q_lo;  // the set computed next
+  uint32_t S = 0;  // the wave's set computed next
   // prologue: records of S .. S + 2 DEPTH - 2, geometry + loads of S .. S + DEPTH - 2
   uint4 Rq[DEPTH];
 #pragma unroll
   for (int i = 0; i < DEPTH; i++) Rq[i] = load_rec(S + i);
 #pragma unroll
   for (int i = 0; i < DEPTH - 1; i++) {
-    GE[i] = geometry(S + i, Rq[i], VO[i], M[i]);
-    load_set(VO[i], GE[i], B[i]);
+    GE[i] = geometry(S + i, Rq[i], VO[i], M[i], SB[i]);
+    load_set(VO[i], GE[i], SB[i], B[i]);
     O[i] = load_rec(S + DEPTH + i);
   }
   O[DEPTH - 1] = Rq[DEPTH - 1];
@@ -390,13 +394,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   // One step: geometry + loads of set S + DEPTH - 1 (record loaded DEPTH steps ago), the record of
   // set S + 2 DEPTH - 1, then compute set S.
   auto step = [&](int cs, int fs) {
-    GE[fs] = geometry(S + DEPTH - 1, O[fs], VO[fs], M[fs]);
-    load_set(VO[fs], GE[fs], B[fs]);
+    GE[fs] = geometry(S + DEPTH - 1, O[fs], VO[fs], M[fs], SB[fs]);
+    load_set(VO[fs], GE[fs], SB[fs], B[fs]);
     O[fs] = load_rec(S + 2 * DEPTH - 1);
     __builtin_amdgcn_sched_barrier(0);
-    if (S < q_end) {
+    if (S < nk) {
       if (!M[cs].slow)
-        compute(S, GE[cs], M[cs], B[cs], VO[cs]);
+        compute(setq(S), GE[cs], M[cs], B[cs], VO[cs], SB[cs]);
       else
         slow_set(S);
     }
@@ -404,13 +408,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     S++;
   };
   if constexpr (DEPTH == 3) {
-    while (S < q_end) {
+    while (S < nk) {
       step(0, 2);
       step(1, 0);
       step(2, 1);
     }
   } else {
-    while (S < q_end) {
+    while (S < nk) {
       step(0, 1);
       step(1, 0);
     }

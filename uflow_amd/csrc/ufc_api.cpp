@@ -319,9 +319,9 @@ int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
 }
 
 // The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): run-sorted records
-// (ufc_dev::sort_runs) into per-stream scratch, then one launch per chunk of < 2^29 frames.
-// Returns UFC_ERR_INVALID_ARG when it does not apply (pairs over a buffer of 2^31 - 2^20 bytes or
-// more: 32-bit offsets), the caller then takes the 4-lane kernel.
+// (ufc_dev::sort_runs) into per-stream scratch, then one launch per chunk of < 2^29 frames.  Any
+// buffer size: each set's loads are relative to the set's own base (a set whose frames lie
+// 2 GB or more apart, possible with pairs, runs on the kernel's byte path).
 int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
   int waves = 12, depth = 2;
 #ifdef UFC_TUNING
@@ -329,7 +329,7 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   if (const char* dp = std::getenv("UFC_V8_DEPTH")) depth = std::atoi(dp);
 #endif
   const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, waves, depth);
-  if (!fn || (pairs && kp.frame_len >= ((uint64_t)1 << 31) - ((uint64_t)1 << 20))) return UFC_ERR_INVALID_ARG;
+  if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain128;
   kp.nib_img = ctx->d_nib32;
   kp.G = ctx->G;
