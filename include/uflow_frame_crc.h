@@ -94,7 +94,10 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 #define UFC_VARLEN_BLOCKSTREAM 5 /*   sorted block-stream kernel (one 1-KB block step at a time) */
 #define UFC_VARLEN_SORTED8 6     /*   sorted runs, 8-frame sets of 8 lanes per frame */
 #define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
-#define UFC_OPT_COUNT_ 3
+#define UFC_OPT_SEAL_KERNEL 3    /* fixed-stride seals: */
+#define UFC_SEAL_TWO_PASS 0      /*   validate kernel's CRC words, then a non-temporal trailer pass (default) */
+#define UFC_SEAL_INLINE 1        /*   trailers written by the CRC kernel itself (round-1/2 default) */
+#define UFC_OPT_COUNT_ 4
 int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value);
 int ufc_ctx_get_option(const ufc_ctx* ctx, int option);
 

@@ -10,6 +10,7 @@ import pytest
 import torch
 
 import oracle
+from uflow_amd import _native as N
 
 pytestmark = pytest.mark.gpu
 
@@ -86,22 +87,29 @@ def test_fixed_kat(engine):
     assert int(valid.cpu()[0]) == 1
 
 
-def test_seal_fixed(engine):
-    rng = np.random.default_rng(11)
-    for frame_len in (4, 5, 9, 14, 25, 259, 260, 1472, 1500, 2051):
-        for stride in (frame_len, frame_len + 5):
-            n = 130
-            buf = _rand_bytes(rng, n * stride + 16)
-            ref = buf.copy()
-            oracle.seal_fixed(ref, stride, frame_len, n)
-            d = torch.from_numpy(buf).to(DEV)
-            crc_out = torch.empty(n, dtype=torch.int32, device=DEV)
-            engine.seal_fixed(d, frame_len, stride=stride, n=n, crc_out=crc_out)
-            torch.cuda.synchronize()
-            assert np.array_equal(d.cpu().numpy(), ref), f"seal len={frame_len} stride={stride}"
-            ref_crc, ref_valid = oracle.validate_fixed(ref, stride, frame_len, n)
-            assert np.array_equal(crc_out.cpu().numpy().view(np.uint32), ref_crc)
-            assert ref_valid.all() or frame_len < 5
+@pytest.mark.parametrize("seal_kernel", ["two_pass", "inline"])
+def test_seal_fixed(engine, seal_kernel):
+    """Both seal variants (UFC_OPT_SEAL_KERNEL), with and without a crc_out (per-stream scratch)."""
+    engine.set_option(N.UFC_OPT_SEAL_KERNEL, N.UFC_SEAL_INLINE if seal_kernel == "inline" else N.UFC_SEAL_TWO_PASS)
+    try:
+        rng = np.random.default_rng(11)
+        for frame_len in (4, 5, 9, 14, 25, 259, 260, 1472, 1500, 2051):
+            for stride in (frame_len, frame_len + 5, frame_len + 3):
+                for n, want_crc in ((130, True), (1001, False)):
+                    buf = _rand_bytes(rng, n * stride + 16)
+                    ref = buf.copy()
+                    oracle.seal_fixed(ref, stride, frame_len, n)
+                    d = torch.from_numpy(buf).to(DEV)
+                    crc_out = torch.empty(n, dtype=torch.int32, device=DEV) if want_crc else None
+                    engine.seal_fixed(d, frame_len, stride=stride, n=n, crc_out=crc_out)
+                    torch.cuda.synchronize()
+                    assert np.array_equal(d.cpu().numpy(), ref), f"seal len={frame_len} stride={stride} n={n}"
+                    ref_crc, ref_valid = oracle.validate_fixed(ref, stride, frame_len, n)
+                    if want_crc:
+                        assert np.array_equal(crc_out.cpu().numpy().view(np.uint32), ref_crc)
+                    assert ref_valid.all() or frame_len < 5
+    finally:
+        engine.set_option(N.UFC_OPT_SEAL_KERNEL, N.UFC_SEAL_TWO_PASS)
 
 
 def _varlen_case(engine, rng, lens, seal=True, flip_every=0):

@@ -82,6 +82,10 @@ const void* varlen8_kernel_symbol(bool seal, bool pairs, int waves, int depth);
 // Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride
 // + lens[i] (ufc_validate_host_slots_async).
 int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream);
+// Seal, second pass (fixed stride): write crc[i] big-endian at i * stride + frame_len - 4 for
+// every frame, non-temporal (frame_len >= 4).  Returns a hipError_t.
+int seal_scatter(uint8_t* bytes, uint64_t stride, uint64_t frame_len, uint64_t nframes, const uint32_t* crc,
+                 void* stream);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

@@ -63,7 +63,7 @@ constexpr uint32_t kCtrSlots = 64;
 
 namespace {
 
-enum ScratchKind { kScratchParse = 0, kScratchSortRec = 1, kScratchAsyncSlots = 2 };
+enum ScratchKind { kScratchParse = 0, kScratchSortRec = 1, kScratchAsyncSlots = 2, kScratchSealCrc = 3 };
 
 // The (kind, stream) scratch buffer of at least `need` bytes.  Growing waits for the work already
 // queued on that stream (the only user of the old buffer) before freeing it.
@@ -464,6 +464,9 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
     case UFC_OPT_GENERIC_JC:
       if (value != 0 && !ufc_dev::config_available(value)) return UFC_ERR_INVALID_ARG;
       break;
+    case UFC_OPT_SEAL_KERNEL:
+      if (value < UFC_SEAL_TWO_PASS || value > UFC_SEAL_INLINE) return UFC_ERR_INVALID_ARG;
+      break;
     default: return UFC_ERR_INVALID_ARG;
   }
   ctx->opt[option] = value;
@@ -524,6 +527,8 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
                                       : std::strcmp(k, "blockstream") == 0 ? UFC_VARLEN_BLOCKSTREAM
                                       : std::strcmp(k, "sorted8") == 0 ? UFC_VARLEN_SORTED8 : UFC_VARLEN_AUTO;
   if (const char* j = std::getenv("UFC_FIXED_JC")) ctx->opt[UFC_OPT_GENERIC_JC] = std::atoi(j);
+  if (const char* k = std::getenv("UFC_SEAL_KERNEL"))
+    ctx->opt[UFC_OPT_SEAL_KERNEL] = std::strcmp(k, "inline") == 0 ? UFC_SEAL_INLINE : UFC_SEAL_TWO_PASS;
 #endif
   *out = ctx;
   return UFC_OK;
@@ -625,8 +630,23 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   kp.nframes = n;
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
-  if (const int lean = lean_fixed_blocks(ctx, frame_len, stride, n))
-    return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
+  if (const int lean = lean_fixed_blocks(ctx, frame_len, stride, n)) {
+    if (ctx->opt[UFC_OPT_SEAL_KERNEL] == UFC_SEAL_INLINE)  // A/B: trailers written by the CRC kernel
+      return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
+    // Two passes: the validate kernel's CRC words (into the caller's
+    // crc_out, or per-stream scratch), then every trailer with non-temporal stores once the whole
+    // batch has been read.
+    uint32_t* crc = d_crc_out;
+    hipError_t e;
+    if (!crc && (e = stream_scratch(ctx, kScratchSealCrc, (hipStream_t)stream, n * 4, (void**)&crc)) != hipSuccess)
+      return hip_fail(ctx, e);
+    kp.wbytes = nullptr;
+    kp.crc_out = crc;
+    if (const int r = launch_lean_fixed(ctx, lean, false, kp, (hipStream_t)stream)) return r;
+    if ((e = (hipError_t)ufc_dev::seal_scatter(d_frames, stride, frame_len, n, crc, stream)) != hipSuccess)
+      return hip_fail(ctx, e);
+    return UFC_OK;
+  }
   return launch(ctx, cfg, freeze | ufc_dev::kModeSeal, kp, (hipStream_t)stream);
 }
 
