@@ -48,6 +48,8 @@ def parse():
                     help="untimed back-to-back launches before the warmup steps: a GPU coming out of idle "
                          "runs ~15%% slower for a few ms (DESIGN.md section 6); the timed steps measure the "
                          "sustained rate")
+    ap.add_argument("--event-every", type=int, default=1,
+                    help="bracket every k-th timed step's gate with HIP events (roofline.kernel_avg_ms)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of each CPU baseline leg")
     return ap.parse_args()
@@ -209,7 +211,9 @@ def main():
         torch.cuda.synchronize(dev)
     for _ in range(a.warmup):
         step()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(a.steps)]
+    ev_every = max(1, a.event_every)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if i % ev_every == 0 else None
+           for i in range(a.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -226,7 +230,7 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_all = np.array([e0.elapsed_time(e1) for e0, e1 in evs])
+    kern_all = np.array([ev[0].elapsed_time(ev[1]) for ev in evs if ev is not None])
     kern_ms = float(np.mean(kern_all))
 
     # ---- correctness (after the timed region) ----
@@ -300,7 +304,9 @@ def main():
                 "kernel_median_ms": round(float(np.median(kern_all)), 4),
                 "kernel_min_ms": round(float(np.min(kern_all)), 4),
                 "algorithmic_bytes_per_launch": algo_bytes,
-                "timed_on": "HIP events on the compute stream around each step's gate"
+                "timed_on": (f"HIP events on the compute stream around the gate of every {ev_every}-th timed step "
+                             f"({kern_all.size} launches)" if ev_every > 1 else
+                             "HIP events on the compute stream around each step's gate")
                             + (" (all chunks of this rank's shard)" if world > 1 else ""),
                 **({"traffic_source": tsrc} if tsrc else {}),
             },

@@ -286,6 +286,96 @@ def test_parse_varlen_vs_oracle(engine):
     assert int(used.cpu()[0]) == total
 
 
+def _parse_edge_batch(seed):
+    """Frames that take each path of the batch parse: data frames with <= 64 datagrams (header
+    slots), 65..127 datagrams and frames over 64 KiB (walked again with direct stores), ack frames
+    (fixed group offsets) with 0..161 groups, syncs, damaged and unsealed frames, all interleaved."""
+    import random
+    from oracle import codec as C
+    rng = random.Random(seed)
+
+    def dg(t, data):
+        a, b = sorted((rng.getrandbits(16), rng.getrandbits(16)))
+        return dict(sequence_id=rng.getrandbits(32) & C.PACKET_ID_MASK, channel_id=rng.randrange(64),
+                    window_parent_lead=rng.randrange(128) if t == 0 else rng.getrandbits(16),
+                    channel_parent_lead=rng.randrange(256) if t == 0 else rng.getrandbits(16),
+                    fragment_id=a if t == 2 else 0, fragment_id_last=b if t == 2 else 0, data=data)
+
+    frames = []
+    for i in range(1500):
+        r = i % 7
+        if r == 0:  # many micro datagrams: 65..127 headers
+            dgs = [dg(0, bytes(rng.getrandbits(8) for _ in range(rng.randrange(3))))
+                   for _ in range(rng.randrange(65, 128))]
+            f = {"kind": "data", "sequence_id": rng.getrandbits(32), "nonce": bool(rng.getrandbits(1)), "datagrams": dgs}
+        elif r == 1 and i % 70 == 1:  # over 64 KiB: large datagrams
+            dgs = [dg(2, bytes(rng.getrandbits(8) for _ in range(rng.randrange(20000, 30000)))) for _ in range(3)]
+            f = {"kind": "data", "sequence_id": rng.getrandbits(32), "nonce": False, "datagrams": dgs}
+        elif r == 2:
+            f = C.random_ack_frame(rng, 162)
+        elif r == 3:
+            f = C.random_data_frame(rng, 64)  # 0..63 datagrams
+        elif r == 4:
+            f = C.random_sync_frame(rng)
+        else:
+            f = C.random_data_frame(rng, 128, 70)
+        fb = bytearray(C.frame_write(f))
+        if i % 11 == 5:
+            fb[rng.randrange(len(fb))] ^= 1 << rng.randrange(8)  # fails the gate
+        elif i % 13 == 6 and len(fb) > 12:
+            fb[rng.randrange(6, min(len(fb) - 4, 40))] = rng.getrandbits(8)  # damaged header, resealed
+            fb[-4:] = oracle.compute(bytes(fb[:-4])).to_bytes(4, "big")
+        frames.append(bytes(fb))
+    offsets = np.zeros(len(frames) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum([len(f) for f in frames])
+    return frames, np.frombuffer(b"".join(frames), dtype=np.uint8).copy(), offsets
+
+
+def test_parse_varlen_slow_paths_and_cap(engine):
+    """Every parse path vs the codec oracle, then the same batch with an item cap that cuts
+    through the middle (items past the cap are not written; item_first / items_used unchanged)."""
+    from oracle import codec as C
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE
+    from test_codec_cpu import info_to_dict
+    frames, data, offsets = _parse_edge_batch(31)
+    d = torch.from_numpy(data).to(DEV)
+    o = torch.from_numpy(offsets).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    infos = infos.cpu().numpy().view(FRAME_INFO_DTYPE).reshape(-1)
+    items = items.cpu().numpy().view(ITEM_DTYPE).reshape(-1)
+    total, walked = 0, 0
+    for i, fb in enumerate(frames):
+        cnt = int(infos[i]["item_count"]) if infos[i]["ok"] else 0
+        assert int(infos[i]["item_first"]) == total
+        assert info_to_dict(infos[i], items[total:total + cnt], fb) == C.frame_read(fb), i
+        walked += int(fb[0] == 10 and (cnt > 64 or len(fb) > 65535))
+        total += cnt
+    assert int(used.cpu()[0]) == total
+    assert walked > 100  # the direct-store path ran
+    cap = total // 2 + 7
+    fill = torch.full((cap + 100, 24), 0xA5, dtype=torch.uint8, device=DEV)
+    infos2, _, used2 = engine.parse_varlen(d, o, valid, items_cap=cap)
+    # (parse_varlen allocates its own item array; run the capped parse into a sentinel-filled one)
+    from uflow_amd import _native as NN
+    import ctypes
+    used3 = torch.zeros(1, dtype=torch.int64, device=DEV)
+    infos3 = torch.empty_like(infos2)
+    rc = NN.lib().ufc_parse_batch_varlen(engine._ctx, ctypes.c_void_p(d.data_ptr()), ctypes.c_void_p(o.data_ptr()),
+                                        len(frames), ctypes.c_void_p(valid.data_ptr()),
+                                        ctypes.c_void_p(infos3.data_ptr()), ctypes.c_void_p(fill.data_ptr()), cap,
+                                        ctypes.c_void_p(used3.data_ptr()),
+                                        ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert int(used3.cpu()[0]) == total and int(used2.cpu()[0]) == total
+    assert np.array_equal(infos3.cpu().numpy().view(FRAME_INFO_DTYPE).reshape(-1), infos)
+    got = fill.cpu().numpy()
+    assert np.array_equal(got[:cap].view(ITEM_DTYPE).reshape(-1), items[:cap])
+    assert (got[cap:] == 0xA5).all()
+
+
 def test_parse_varlen_vs_host_parse_large(engine):
     """A 200k-frame batch: device parse == host parse (itself pinned to the oracle on CPU)."""
     from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host

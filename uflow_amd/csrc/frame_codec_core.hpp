@@ -42,11 +42,74 @@ UFC_HD bool datagram_is_valid(const ufc_item& d) {
   return true;
 }
 
+// A datagram header (read_datagram, serial/mod.rs:183-309) from a header reader h(c) = byte c of
+// the header: its size hs (micro 6, small 9, large 14) and payload length dl (reads byte 0, and 1-2
+// for small / large) ...
+template <class H>
+UFC_HD void datagram_size(const H& h, uint32_t& hs, uint32_t& dl) {
+  const uint32_t b0 = h(0);
+  if ((b0 & 0x80) == 0) {  // micro (:190-229)
+    hs = 6;
+    dl = b0 & 0x3F;
+  } else if ((b0 & 0x40) == 0) {  // small (:230-268)
+    hs = 9;
+    dl = h(1);
+  } else {  // large (:269-308)
+    hs = 14;
+    dl = (h(1) << 8) | h(2);
+  }
+}
+
+// ... and its fields, once the frame is known to hold hs + dl bytes from the header on.
+// data_offset is left to the caller (the header's frame offset + hs).
+template <class H>
+UFC_HD void decode_datagram(const H& h, uint32_t hs, ufc_item& it) {
+  const uint32_t b0 = h(0);
+  if (hs == 6) {  // micro
+    const uint32_t b1 = h(1), b4d = h(4);
+    it.channel_id = (uint8_t)(((b4d >> 2) & 0x20) | ((b0 >> 2) & 0x10) | (b1 & 0x0F));
+    it.id = ((b1 & 0xF0) << 12) | (h(2) << 8) | h(3);
+    it.window_parent_lead = (uint16_t)(b4d & 0x7F);
+    it.channel_parent_lead = (uint16_t)h(5);
+    it.form = 0;
+    it.data_len = b0 & 0x3F;
+  } else if (hs == 9) {  // small
+    it.channel_id = (uint8_t)(b0 & 0x3F);
+    it.id = ((h(2) & 0x0F) << 16) | (h(3) << 8) | h(4);
+    it.window_parent_lead = (uint16_t)((h(5) << 8) | h(6));
+    it.channel_parent_lead = (uint16_t)((h(7) << 8) | h(8));
+    it.form = 1;
+    it.data_len = h(1);
+  } else {  // large
+    it.channel_id = (uint8_t)(b0 & 0x3F);
+    it.id = ((h(3) & 0x0F) << 16) | (h(4) << 8) | h(5);
+    it.window_parent_lead = (uint16_t)((h(6) << 8) | h(7));
+    it.channel_parent_lead = (uint16_t)((h(8) << 8) | h(9));
+    it.fragment_id = (uint16_t)((h(10) << 8) | h(11));
+    it.fragment_id_last = (uint16_t)((h(12) << 8) | h(13));
+    it.form = 2;
+    it.data_len = (h(1) << 8) | h(2);
+  }
+  it.flags = datagram_is_valid(it) ? UFC_ITEM_VALID : 0;
+}
+
+// An ack group (serial/mod.rs:395-417) from h(c) = byte c of the group.
+template <class H>
+UFC_HD void decode_ack_group(const H& h, ufc_item& it) {
+  it.id = (h(0) << 24) | (h(1) << 16) | (h(2) << 8) | h(3);
+  it.data_offset = (h(4) << 24) | (h(5) << 16) | (h(6) << 8) | h(7);  // bitfield
+  it.channel_id = (uint8_t)(h(8) != 0 ? 1 : 0);
+  it.form = 3;
+}
+
 // Where the items go: sink(k, item) for k < cap, when sink.on().  PtrSink: a plain array.
+// kDecode false: the sink only takes each datagram header's frame offset, header(k, off).
 struct PtrSink {
+  static constexpr bool kDecode = true;
   ufc_item* p;
   UFC_HD bool on() const { return p != nullptr; }
   UFC_HD void operator()(uint32_t k, const ufc_item& it) const { p[k] = it; }
+  UFC_HD void header(uint32_t, uint32_t) const {}
 };
 
 // Parse the payload of a frame of `len` bytes (len >= 5) whose CRC gate passed.  Fills `info`
@@ -94,44 +157,20 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, cons
       for (uint32_t k = 0; k < cnt; k++) {  // read_datagram, :183-309
         const uint32_t rem = plen - pos;
         if (rem < 6) return false;
-        const uint32_t b0 = p(pos);
-        ufc_item it{};
+        auto h = [&](uint32_t c) -> uint32_t { return p(pos + c); };
         uint32_t hs, dl;
-        if ((b0 & 0x80) == 0) {  // micro (:190-229)
-          hs = 6;
-          dl = b0 & 0x3F;
-          if (rem < hs + dl) return false;
-          const uint32_t b1 = p(pos + 1), b4d = p(pos + 4);
-          it.channel_id = (uint8_t)(((b4d >> 2) & 0x20) | ((b0 >> 2) & 0x10) | (b1 & 0x0F));
-          it.id = ((b1 & 0xF0) << 12) | (p(pos + 2) << 8) | p(pos + 3);
-          it.window_parent_lead = (uint16_t)(b4d & 0x7F);
-          it.channel_parent_lead = (uint16_t)p(pos + 5);
-          it.form = 0;
-        } else if ((b0 & 0x40) == 0) {  // small (:230-268)
-          hs = 9;
-          dl = p(pos + 1);
-          if (rem < hs + dl) return false;
-          it.channel_id = (uint8_t)(b0 & 0x3F);
-          it.id = ((p(pos + 2) & 0x0F) << 16) | (p(pos + 3) << 8) | p(pos + 4);
-          it.window_parent_lead = (uint16_t)p16(pos + 5);
-          it.channel_parent_lead = (uint16_t)p16(pos + 7);
-          it.form = 1;
-        } else {  // large (:269-308)
-          hs = 14;
-          dl = p16(pos + 1);
-          if (rem < hs + dl) return false;
-          it.channel_id = (uint8_t)(b0 & 0x3F);
-          it.id = ((p(pos + 3) & 0x0F) << 16) | (p(pos + 4) << 8) | p(pos + 5);
-          it.window_parent_lead = (uint16_t)p16(pos + 6);
-          it.channel_parent_lead = (uint16_t)p16(pos + 8);
-          it.fragment_id = (uint16_t)p16(pos + 10);
-          it.fragment_id_last = (uint16_t)p16(pos + 12);
-          it.form = 2;
+        datagram_size(h, hs, dl);
+        if (rem < hs + dl) return false;
+        if (items.on() && k < cap) {
+          if (Sink::kDecode) {
+            ufc_item it{};
+            decode_datagram(h, hs, it);
+            it.data_offset = 1 + pos + hs;
+            items(k, it);
+          } else {
+            items.header(k, 1 + pos);  // the header's frame offset only
+          }
         }
-        it.data_offset = 1 + pos + hs;
-        it.data_len = dl;
-        it.flags = datagram_is_valid(it) ? UFC_ITEM_VALID : 0;
-        if (items.on() && k < cap) items(k, it);
         pos += hs + dl;
       }
       if (pos != plen) return false;  // :335-337
@@ -153,14 +192,11 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, cons
       if (plen - kAckPayloadHeader != UFC_ACK_GROUP_SIZE * cnt) return false;
       info.f[0] = p32(0);
       info.f[1] = p32(4);
-      if (items.on()) {
+      if (items.on() && Sink::kDecode) {  // (ack groups sit at fixed offsets: no header hook)
         for (uint32_t k = 0; k < cnt && k < cap; k++) {
           const uint32_t o = kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
           ufc_item it{};
-          it.id = p32(o);
-          it.data_offset = p32(o + 4);  // bitfield
-          it.channel_id = (uint8_t)(p(o + 8) != 0 ? 1 : 0);
-          it.form = 3;
+          decode_ack_group([&](uint32_t c) -> uint32_t { return p(o + c); }, it);
           items(k, it);
         }
       }

@@ -1,15 +1,24 @@
 // frame_parse.hip -- batched Frame::read after the batched CRC gate, on device-resident frames
 // (on-GPU datagram header parse/validation).
 //
-// One thread per frame runs the payload parse of frame_codec_core.hpp (restating
-// src/frame/serial/mod.rs:54-434, 694-705) over the frame's bytes in HBM: only header bytes are
-// read (a datagram header, then a jump over its payload), by independent byte loads the compiler
-// issues together (a 16-byte chunk cache in registers measured slower: its per-lane misses
-// diverge).  Items leave as three 8-byte stores each.  Three steps on the caller's stream:
-//   1. count:  gate (the CRC kernel's valid flag) + parse -> item count per frame;
-//   2. scan:   exclusive sum of the item counts (hipcub) -> each frame's first item;
-//   3. fill:   parse again, write the frame's ufc_frame_info and its items (datagram / ack group
-//              descriptors) at its first index; the total goes to *items_used.
+// Three steps on the caller's stream, workgroups of 256 frames (one thread per frame):
+//   1. walk:  gate + parse of frame_codec_core.hpp (restating src/frame/serial/mod.rs:54-434,
+//             694-705) -> the frame's ufc_frame_info (item_first aside), its item count, a mode
+//             byte and, for data frames, the frame offsets of its datagram headers: u16 slots in
+//             LDS while the thread walks (no global store inside the dependent load chain), then
+//             written compactly per workgroup.  Only the bytes the walk needs are read (each
+//             datagram's first byte and its length bytes).
+//   2. scan:  exclusive sum of the item counts (hipcub) -> each frame's first item.
+//   3. emit:  item-parallel over the workgroup's item range: lane j finds its frame (binary search
+//             over the firsts in LDS), loads the header bytes (independent 4-byte loads across
+//             items), decodes the ufc_item (datagram with datagram_is_valid of
+//             packet_receiver/mod.rs:12-30, or ack group) and stores it: consecutive lanes write
+//             consecutive 24-byte records.  Frames whose headers did not fit the slots (more than
+//             kPosSlots datagrams, or longer than 64 KiB) are walked again by their own thread,
+//             storing directly.
+// Round-1 shape (one thread walking and storing every item, 1.18 ms for 1M frames): every item
+// store sat in the same vmcnt queue as the walk's next header load, and the stores of a wave
+// scattered over 64 frames' item ranges.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -22,11 +31,27 @@ namespace ufc_dev {
 
 namespace {
 
+constexpr int kParseThreads = 256;
+constexpr uint32_t kPosSlots = 64;  // datagram headers recorded per frame (a data frame holds <= 127)
+constexpr uint64_t kSegWords = (uint64_t)kPosSlots * kParseThreads;  // u16 per workgroup segment
+enum : uint8_t { kItemsNone = 0, kItemsPos = 1, kItemsAck = 2, kItemsWalk = 3 };
+
+typedef hipcub::BlockScan<uint32_t, kParseThreads> BlockScan;
+
 struct DevBytes {
   const uint8_t* p;
   __device__ uint32_t operator()(uint32_t i) const {
     return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
   }
+};
+
+// Walk sink: only the header offsets, into this thread's LDS slots (slot k at k * kParseThreads).
+struct PosSink {
+  static constexpr bool kDecode = false;
+  uint16_t* slot;
+  __device__ bool on() const { return true; }
+  __device__ void operator()(uint32_t, const ufc_item&) const {}
+  __device__ void header(uint32_t k, uint32_t off) const { slot[k * kParseThreads] = (uint16_t)off; }
 };
 
 // Items as three 8-byte stores each (ufc_item is 24 bytes, laid out as below).
@@ -36,18 +61,21 @@ static_assert(sizeof(ufc_item) == 24 && offsetof(ufc_item, channel_id) == 4 && o
                   offsetof(ufc_item, flags) == 14 && offsetof(ufc_item, data_offset) == 16 &&
                   offsetof(ufc_item, data_len) == 20,
               "ufc_item layout");
+__device__ __forceinline__ void store_item(ufc_item* p, const ufc_item& it) {
+  typedef __attribute__((address_space(1))) uint64_t g_u64w;
+  g_u64w* q = (g_u64w*)p;
+  q[0] = (uint64_t)it.id | ((uint64_t)it.channel_id << 32) | ((uint64_t)it.form << 40) |
+         ((uint64_t)it.window_parent_lead << 48);
+  q[1] = (uint64_t)it.channel_parent_lead | ((uint64_t)it.fragment_id << 16) | ((uint64_t)it.fragment_id_last << 32) |
+         ((uint64_t)it.flags << 48);
+  q[2] = (uint64_t)it.data_offset | ((uint64_t)it.data_len << 32);
+}
 struct PackedSink {
+  static constexpr bool kDecode = true;
   ufc_item* p;
   __device__ bool on() const { return p != nullptr; }
-  __device__ void operator()(uint32_t k, const ufc_item& it) const {
-    typedef __attribute__((address_space(1))) uint64_t g_u64w;
-    g_u64w* q = (g_u64w*)((uint8_t*)(p + k));
-    q[0] = (uint64_t)it.id | ((uint64_t)it.channel_id << 32) | ((uint64_t)it.form << 40) |
-           ((uint64_t)it.window_parent_lead << 48);
-    q[1] = (uint64_t)it.channel_parent_lead | ((uint64_t)it.fragment_id << 16) |
-           ((uint64_t)it.fragment_id_last << 32) | ((uint64_t)it.flags << 48);
-    q[2] = (uint64_t)it.data_offset | ((uint64_t)it.data_len << 32);
-  }
+  __device__ void operator()(uint32_t k, const ufc_item& it) const { store_item(p + k, it); }
+  __device__ void header(uint32_t, uint32_t) const {}
 };
 
 __device__ __forceinline__ uint32_t frame_len32(const uint64_t* offsets, uint64_t i, uint64_t& a) {
@@ -57,33 +85,144 @@ __device__ __forceinline__ uint32_t frame_len32(const uint64_t* offsets, uint64_
   return len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
 }
 
-__global__ __launch_bounds__(256) void parse_count_kernel(const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
-                                                          const uint8_t* valid, uint32_t* counts) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint64_t a;
-  const uint32_t len = frame_len32(offsets, i, a);
-  ufc_frame_info info;
-  const bool ok = ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[i] != 0, info, PackedSink{nullptr}, 0);
-  counts[i] = ok ? info.item_count : 0u;
+__global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t* bytes, const uint64_t* offsets,
+                                                                   uint64_t n, const uint8_t* valid,
+                                                                   ufc_frame_info* infos, uint32_t* counts,
+                                                                   uint8_t* modes, uint16_t* pos_seg) {
+  __shared__ uint16_t slots[kSegWords];
+  __shared__ typename BlockScan::TempStorage scan_tmp;
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + t;
+  uint32_t npos = 0;
+  if (i < n) {
+    uint64_t a;
+    const uint32_t len = frame_len32(offsets, i, a);
+    ufc_frame_info info;
+    const bool ok = ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[i] != 0, info, PosSink{slots + t},
+                                             kPosSlots);
+    const uint32_t cnt = ok ? info.item_count : 0u;
+    uint8_t mode = kItemsNone;
+    if (cnt) {
+      if (info.kind == UFC_FRAME_ACK) {
+        mode = kItemsAck;
+      } else if (cnt <= kPosSlots && len <= 0xFFFFu) {
+        mode = kItemsPos;
+        npos = cnt;
+      } else {
+        mode = kItemsWalk;
+      }
+    }
+    info.item_first = 0;  // written by the emit step
+    infos[i] = info;
+    counts[i] = cnt;
+    modes[i] = mode;
+  }
+  uint32_t lo;
+  BlockScan(scan_tmp).ExclusiveSum(npos, lo);
+  // (each thread reads back only the slots it wrote)
+  uint16_t* seg = pos_seg + (uint64_t)blockIdx.x * kSegWords;
+  for (uint32_t k = 0; k < npos; k++) seg[lo + k] = slots[k * kParseThreads + t];
 }
 
-__global__ __launch_bounds__(256) void parse_fill_kernel(const uint8_t* bytes, const uint64_t* offsets, uint64_t n,
-                                                         const uint8_t* valid, ufc_frame_info* infos,
-                                                         const uint32_t* counts, const uint32_t* firsts,
-                                                         ufc_item* items, uint64_t cap, uint64_t* items_used) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t first = firsts[i], cnt = counts[i];
-  if (i == n - 1 && items_used) *items_used = (uint64_t)first + cnt;
-  uint64_t a;
-  const uint32_t len = frame_len32(offsets, i, a);
-  const uint32_t room = (cnt == 0 || !items || (uint64_t)first >= cap) ? 0u : (uint32_t)min((uint64_t)cnt, cap - first);
-  ufc_frame_info info;
-  ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[i] != 0, info, PackedSink{room ? items + first : nullptr},
-                           room);
-  info.item_first = first;
-  infos[i] = info;
+__global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
+    const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
+    const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg, ufc_item* items,
+    uint64_t cap, uint64_t* items_used) {
+  __shared__ uint32_t lfirst[kParseThreads], lseg[kParseThreads];
+  __shared__ uint64_t lstart[kParseThreads];
+  __shared__ uint8_t lmode[kParseThreads];
+  __shared__ uint32_t lend;
+  __shared__ typename BlockScan::TempStorage scan_tmp;
+  const uint32_t t = threadIdx.x;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kParseThreads, i = i0 + t;
+  const uint32_t nb = (uint32_t)min((uint64_t)kParseThreads, n - i0);  // frames of this workgroup
+  uint32_t first = 0, cnt = 0;
+  uint8_t mode = kItemsNone;
+  uint64_t a = 0;
+  if (i < n) {
+    first = firsts[i];
+    cnt = counts[i];
+    mode = modes[i];
+    a = offsets[i];
+    infos[i].item_first = first;
+    if (i == n - 1 && items_used) *items_used = (uint64_t)first + cnt;
+  }
+  uint32_t lo;
+  BlockScan(scan_tmp).ExclusiveSum(mode == kItemsPos ? cnt : 0u, lo);
+  lfirst[t] = first;
+  lseg[t] = lo;
+  lstart[t] = a;
+  lmode[t] = mode;
+  if (t == nb - 1) lend = first + cnt;
+  __syncthreads();
+
+  // Header bytes through a buffer resource over the workgroup's bytes (4-byte aligned base, range
+  // rounded up to whole dwords: a dword holding a frame byte never leaves that byte's page); five
+  // dword loads cover 16 bytes from any offset.  Spans of 4 GiB and more take byte loads.
+  const uint64_t span_lo = lstart[0];
+  const uint64_t span_hi = offsets[i0 + nb];
+  const uintptr_t base_addr = (uintptr_t)(bytes + span_lo);
+  const uint32_t delta = (uint32_t)(base_addr & 3u);
+  const uint64_t range = (span_hi - span_lo + delta + 3) & ~(uint64_t)3;
+  const bool buf_ok = span_hi >= span_lo && range < 0xFFFFFFF0ull;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(base_addr - delta), 0, buf_ok ? (int)(uint32_t)range : 0, 0x00020000);
+
+  const uint32_t g0 = lfirst[0], g1 = lend;
+  const uint16_t* seg = pos_seg + (uint64_t)blockIdx.x * kSegWords;
+  if (items) {
+    for (uint32_t g = g0 + t; g < g1 && (uint64_t)g < cap; g += kParseThreads) {
+      uint32_t lo_f = 0, hi_f = nb - 1;  // owner: the last frame whose first item is <= g
+      while (lo_f < hi_f) {
+        const uint32_t mid = (lo_f + hi_f + 1) >> 1;
+        if (lfirst[mid] <= g)
+          lo_f = mid;
+        else
+          hi_f = mid - 1;
+      }
+      const uint32_t f = lo_f, k = g - lfirst[f];
+      const uint8_t m = lmode[f];
+      if (m != kItemsPos && m != kItemsAck) continue;
+      const uint32_t hoff = m == kItemsPos ? (uint32_t)seg[lseg[f] + k]
+                                           : 1u + ufc_codec::kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
+      uint32_t w[4];
+      if (buf_ok) {
+        const uint32_t rel = (uint32_t)(lstart[f] - span_lo) + delta + hoff;
+        const uint32_t al = rel & ~3u, sh = rel & 3u;
+        uint32_t x[5];
+#pragma unroll
+        for (int q = 0; q < 5; q++) x[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(al + 4 * q), 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbyte(x[q + 1], x[q], sh);
+      } else {
+        const DevBytes rd{bytes + lstart[f] + hoff};
+#pragma unroll
+        for (int q = 0; q < 4; q++) w[q] = 0;
+        // (only the bytes the header occupies: a datagram's hs <= 14, an ack group 9)
+        const uint32_t nbytes = m == kItemsAck ? UFC_ACK_GROUP_SIZE : 14u;
+        for (uint32_t c = 0; c < nbytes; c++) w[c >> 2] |= rd(c) << (8 * (c & 3));
+      }
+      auto h = [&](uint32_t c) -> uint32_t { return (w[c >> 2] >> (8 * (c & 3))) & 0xFFu; };
+      ufc_item it{};
+      if (m == kItemsPos) {
+        uint32_t hs, dl;
+        ufc_codec::datagram_size(h, hs, dl);
+        ufc_codec::decode_datagram(h, hs, it);
+        it.data_offset = hoff + hs;
+      } else {
+        ufc_codec::decode_ack_group(h, it);
+      }
+      store_item(items + g, it);
+    }
+    // Frames whose headers did not fit the slots: walked again, items stored directly.
+    if (mode == kItemsWalk && (uint64_t)first < cap) {
+      uint64_t aa;
+      const uint32_t len = frame_len32(offsets, i, aa);
+      const uint32_t room = (uint32_t)min((uint64_t)cnt, cap - first);
+      ufc_frame_info info;
+      ufc_codec::read_frame_to(DevBytes{bytes + aa}, len, valid[i] != 0, info, PackedSink{items + first}, room);
+    }
+  }
 }
 
 }  // namespace
@@ -91,24 +230,32 @@ __global__ __launch_bounds__(256) void parse_fill_kernel(const uint8_t* bytes, c
 size_t parse_scratch_bytes(uint64_t n) {
   size_t temp = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-  return 2 * ((n * 4 + 255) / 256 * 256) + (temp + 255) / 256 * 256;
+  const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
+  auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
+  return 2 * up(n * 4) + up(n) + up(blocks * kSegWords * 2) + up(temp);
 }
 
 hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, hipStream_t stream) {
   const uint64_t n = a.n;
-  const size_t arr = (n * 4 + 255) / 256 * 256;
-  uint32_t* counts = (uint32_t*)scratch;
-  uint32_t* firsts = (uint32_t*)((char*)scratch + arr);
-  void* temp = (char*)scratch + 2 * arr;
-  size_t temp_bytes = scratch_bytes - 2 * arr;
-  const unsigned grid = (unsigned)((n + 255) / 256);
-  parse_count_kernel<<<grid, 256, 0, stream>>>(a.bytes, a.offsets, n, a.valid, counts);
+  const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
+  auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
+  char* s = (char*)scratch;
+  uint32_t* counts = (uint32_t*)s;
+  uint32_t* firsts = (uint32_t*)(s + up(n * 4));
+  uint8_t* modes = (uint8_t*)(s + 2 * up(n * 4));
+  uint16_t* pos_seg = (uint16_t*)(s + 2 * up(n * 4) + up(n));
+  const size_t fixed = 2 * up(n * 4) + up(n) + up(blocks * kSegWords * 2);
+  void* temp = s + fixed;
+  size_t temp_bytes = scratch_bytes - fixed;
+  parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
+                                                                    modes, pos_seg);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
   if (e != hipSuccess) return e;
-  parse_fill_kernel<<<grid, 256, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts, firsts, a.items,
-                                              a.items_cap, a.items_used);
+  parse_emit_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
+                                                                    firsts, modes, pos_seg, a.items, a.items_cap,
+                                                                    a.items_used);
   return hipGetLastError();
 }
 
