@@ -139,8 +139,17 @@ def seal(eng, dev, reps, n=1_000_000, L=1500):
     ok = int(valid.sum()) == n
     settle(fn)
     med, mean = timed(fn, reps)
-    return rates("2 (encode side): seal 1M x 1500-B frames in place, device-resident", n * L, n * L + 4 * n,
-                 med, mean, frames=n, valid_after_seal=ok)
+    # the round-1/2 shape for comparison: trailers written by the CRC kernel itself
+    from uflow_amd import _native as N
+    eng.set_option(N.UFC_OPT_SEAL_KERNEL, N.UFC_SEAL_INLINE)
+    try:
+        settle(fn)
+        med_inline, _ = timed(fn, reps)
+    finally:
+        eng.set_option(N.UFC_OPT_SEAL_KERNEL, N.UFC_SEAL_TWO_PASS)
+    return rates("2 (encode side): seal 1M x 1500-B frames in place, device-resident (two passes: CRC words, "
+                 "then non-temporal trailer stores)", n * L, n * L + 4 * n,
+                 med, mean, frames=n, valid_after_seal=ok, inline_seal_ms=round(med_inline, 4))
 
 
 def parse(eng, dev, reps, n=1_000_000):

@@ -34,4 +34,6 @@ step cfg_write 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/cfg_wr
     python3 $R/tools/bench_configs.py --only $ONLY --reps 3
 step configs 600 python3 $R/tools/bench_configs.py --reps 20
 cat $OUT/configs.log
+timeout -k 10 300 python3 $R/bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -5 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json
 echo done

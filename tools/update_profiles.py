@@ -18,10 +18,11 @@ BENCH_KERNEL = "fixed_kernel<6, false"
 CFG_KERNELS = {
     "varlen (config 3): 8-lane sorted-runs kernel": "frame_crc_varlen8_kernel<false, false",
     "varlen (config 3): its sort pre-pass": "sort_runs_kernel<false>",
-    "seal (config 2 encode side)": "fixed_kernel<6, true",
-    "validate, fixed 1500 B (config 2 in bench; config-4 shard in bench_configs)": "fixed_kernel<6, false",
-    "parse: count": "parse_count",
-    "parse: fill": "parse_fill",
+    "seal (config 2 encode side), pass 2: non-temporal trailer stores": "seal_scatter_kernel",
+    "validate, fixed 1500 B (config 2 in bench; config-4 shard and the seal's pass 1 in bench_configs)":
+        "fixed_kernel<6, false",
+    "parse: walk": "parse_walk",
+    "parse: emit": "parse_emit",
 }
 
 
@@ -80,7 +81,7 @@ def main():
     summary["_note"] = ("avg/min/max from rocprofv3 --kernel-trace --stats of tools/bench_configs.py --only "
                         "varlen,shard,seal,parse --reps 10 (several workloads per kernel name are averaged "
                         "together: the fixed validate kernel runs config 4's shard there, 3 launches of 12.5M/3 "
-                        "frames); FETCH_SIZE KiB x1024 x2 (gfx950 correction), WRITE_SIZE KiB x1024, per dispatch, "
+                        "frames, and the seal's first pass, 1M frames); FETCH_SIZE KiB x1024 x2 (gfx950 correction), WRITE_SIZE KiB x1024, per dispatch, "
                         "from separate --pmc passes (--reps 3)")
     with open(os.path.join(dst, f"{prefix}_kernels.json"), "w") as f:
         json.dump(summary, f, indent=1)
