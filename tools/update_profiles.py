@@ -60,6 +60,21 @@ def main():
     for s, d in copies.items():
         if os.path.exists(os.path.join(src, s)):
             shutil.copy(os.path.join(src, s), os.path.join(dst, f"{prefix}_{d}"))
+    # the bench kernel's dispatches of the timed steps (the trace's last `steps` dispatches: the
+    # settle and warmup launches before them include cold-GPU ones)
+    tr = os.path.join(src, "bench_ktrace", "run_kernel_trace.csv")
+    if os.path.exists(tr):
+        with open(tr) as f:
+            durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in csv.DictReader(f)
+                    if BENCH_KERNEL in r["Kernel_Name"]]
+        steps = 20  # tools/gpu_profile.sh: bench.py --steps 20
+        timed = durs[-steps:]
+        with open(os.path.join(dst, f"{prefix}_bench_timed_dispatches.json"), "w") as f:
+            json.dump({"kernel": BENCH_KERNEL, "dispatches_in_trace": len(durs), "timed_steps": steps,
+                       "timed_avg_us": round(sum(timed) / len(timed), 2), "all_avg_us": round(sum(durs) / len(durs), 2),
+                       "timed_us": [round(x, 1) for x in timed],
+                       "source": "rocprofv3 --kernel-trace of `python3 bench.py --steps 20 --warmup 5 "
+                                 "--no-cpu-baseline` (tools/gpu_profile.sh), End - Start per dispatch"}, f, indent=1)
     bench_path = os.path.join(src, "bench.json")
     bench = last_json(bench_path if os.path.exists(bench_path) else os.path.join(src, "bench_ktrace.log"))
     with open(os.path.join(dst, f"{prefix}_bench.json"), "w") as f:
