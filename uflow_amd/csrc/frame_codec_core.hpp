@@ -43,20 +43,21 @@ UFC_HD bool datagram_is_valid(const ufc_item& d) {
 }
 
 // A datagram header (read_datagram, serial/mod.rs:183-309) from a header reader h(c) = byte c of
-// the header: its size hs (micro 6, small 9, large 14) and payload length dl (reads byte 0, and 1-2
-// for small / large) ...
+// the header: its size hs (micro 6, small 9, large 14) and payload length dl (bytes 0..2) ...
+// The three bytes are read together (one dependent step per datagram in a walk, not two): the
+// callers have checked that at least 6 header bytes remain.
 template <class H>
 UFC_HD void datagram_size(const H& h, uint32_t& hs, uint32_t& dl) {
-  const uint32_t b0 = h(0);
+  const uint32_t b0 = h(0), b1 = h(1), b2 = h(2);
   if ((b0 & 0x80) == 0) {  // micro (:190-229)
     hs = 6;
     dl = b0 & 0x3F;
   } else if ((b0 & 0x40) == 0) {  // small (:230-268)
     hs = 9;
-    dl = h(1);
+    dl = b1;
   } else {  // large (:269-308)
     hs = 14;
-    dl = (h(1) << 8) | h(2);
+    dl = (b1 << 8) | b2;
   }
 }
 

@@ -32,7 +32,10 @@ namespace ufc_dev {
 namespace {
 
 constexpr int kParseThreads = 256;
-constexpr uint32_t kPosSlots = 64;  // datagram headers recorded per frame (a data frame holds <= 127)
+#ifndef UFC_POS_SLOTS
+#define UFC_POS_SLOTS 64
+#endif
+constexpr uint32_t kPosSlots = UFC_POS_SLOTS;  // datagram headers recorded per frame (a data frame holds <= 127)
 constexpr uint64_t kSegWords = (uint64_t)kPosSlots * kParseThreads;  // u16 per workgroup segment
 enum : uint8_t { kItemsNone = 0, kItemsPos = 1, kItemsAck = 2, kItemsWalk = 3 };
 
