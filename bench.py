@@ -51,9 +51,27 @@ def parse():
     ap.add_argument("--event-group", type=int, default=10,
                     help="HIP events around each group of k back-to-back timed gates (roofline.kernel_avg_ms = "
                          "group time / k; 1 = events around every gate, which adds ~6 us per step)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="take the N > 1 path (ufc_crc_sharded over RCCL, gather to rank 0, sampled oracle check) "
+                         "even at N = 1: a one-GPU rehearsal of the driver's multi-GPU run")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of each CPU baseline leg")
     return ap.parse_args()
+
+
+class _StdoutToStderr:
+    """fd 1 -> fd 2 for the duration (RCCL prints its version banner on stdout at communicator
+    creation; the driver reads rank 0's stdout for the one JSON line)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
 
 
 def shard_of(total, rank, world):
@@ -145,10 +163,15 @@ def main():
         print(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run "
               f"--nproc-per-node {a.gpus}", file=sys.stderr)
         sys.exit(2)
+    sharded = world > 1 or a.sharded
+    if sharded and world == 1:  # a one-rank group without a launcher
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm: barriers and the timing max
+    if sharded:
+        with _StdoutToStderr():
+            dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm: barriers and the timing max
 
     from uflow_amd import synth
     from uflow_amd.batch import FrameCrcEngine
@@ -160,29 +183,30 @@ def main():
         total, scaling = a.frames_per_gpu * world, "weak"
     elif a.global_frames is not None:
         total, scaling = a.global_frames, "strong"
-    elif world == 1:
+    elif not sharded:
         total, scaling = 1_000_000, "weak"  # config 2
     else:
         total, scaling = CONFIG4_FRAMES, "strong"  # config 4
-    seed = synth.SEED_CONFIG2 if world == 1 else synth.SEED_CONFIG4
+    seed = synth.SEED_CONFIG2 if not sharded else synth.SEED_CONFIG4
     lo, hi = shard_of(total, rank, world)
     n = hi - lo
     frames = make_frames(eng, lo, n, L, seed, a.flip_every, dev)
 
     gate = None
-    if world > 1:
+    if sharded:
         idt = torch.zeros(128, dtype=torch.uint8, device=dev)
         if rank == 0:
             idt.copy_(torch.frombuffer(bytearray(comm_id_create()), dtype=torch.uint8))
-        dist.broadcast(idt, src=0)
-        gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
+        with _StdoutToStderr():
+            dist.broadcast(idt, src=0)
+            gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
     # Outputs: two slots (step k writes slot k % 2 while the gather of step k - 1 may still read the
     # other); rank 0's slots hold the whole batch in global order.
     n_out = total if rank == 0 else n
     slots = [(torch.empty(n_out, dtype=torch.int32, device=dev), torch.empty(n_out, dtype=torch.uint8, device=dev))
-             for _ in range(2 if world > 1 else 1)]
+             for _ in range(2 if sharded else 1)]
     compute = torch.cuda.current_stream(dev)
-    gather = torch.cuda.Stream(dev) if world > 1 else None
+    gather = torch.cuda.Stream(dev) if sharded else None
     gathered = [None, None]  # event on the gather stream after each slot's last gather
     k_step = [0]
 
@@ -222,7 +246,7 @@ def main():
         evs[g0] = (e0, None) if g1 - g0 > 1 else (e0, e1)
         if g1 - g0 > 1:
             evs[g1 - 1] = (None, e1)
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -230,11 +254,11 @@ def main():
     for i in range(a.steps):
         last = step(evs[i])
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if sharded:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if sharded:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -249,7 +273,7 @@ def main():
         h_valid = valid.cpu().numpy()
         ok = bool(np.array_equal(h_valid, expected_valid(0, total, a.flip_every)))
         h_crc = crc.cpu().numpy().view(np.uint32)
-        if world == 1:
+        if not sharded:
             host = frames.cpu().numpy()
             ref_crc, ref_valid = oracle.validate_fixed_mt(host, L, L, n, min(64, affinity_cpus()))
             exact = bool(np.array_equal(h_crc, ref_crc) and np.array_equal(h_valid, ref_valid))
@@ -275,10 +299,10 @@ def main():
     if rank == 0:
         algo_bytes = n * L + n * 4 + n * 1  # per launch group: frames read + crc words + valid bytes
         achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-        traffic, tsrc = traffic_from_profile(n, L) if world == 1 else (None, None)
+        traffic, tsrc = traffic_from_profile(n, L) if not sharded else (None, None)
         value = total * L / elapsed * a.steps / 2**30
         cfg_name = (f"config 2 (BASELINE.json configs[1]): {n} x {L}-B frames, fixed stride, device-resident"
-                    if world == 1 and total == 1_000_000 else
+                    if not sharded and total == 1_000_000 else
                     f"config 4 (BASELINE.json configs[3]): {total} x {L}-B frames sharded over {world} GPUs "
                     f"({n} per GPU on rank 0), RCCL gather of every CRC word + valid flag to rank 0 in global "
                     f"order (ufc_crc_sharded)" if total == CONFIG4_FRAMES else
@@ -307,23 +331,24 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8> (ufc_crc_batch_fixed"
-                          + (", per chunk of ufc_crc_sharded" if world > 1 else "") + ")",
+                          + (", per chunk of ufc_crc_sharded" if sharded else "") + ")",
                 "kernel_avg_ms": round(kern_ms, 4),
                 "kernel_median_ms": round(float(np.median(kern_all)), 4),
                 "kernel_min_ms": round(float(np.min(kern_all)), 4),
                 "algorithmic_bytes_per_launch": algo_bytes,
-                "timed_on": (f"HIP events on the compute stream around {len(groups)} groups of {G} back-to-back "
-                             "gates (per-launch average, inter-launch gaps included)" if G > 1 else
+                "timed_on": (f"HIP events on the compute stream around {len(groups)} group(s) of up to "
+                             f"{min(G, a.steps)} back-to-back gates (per-launch average, inter-launch gaps "
+                             "included)" if G > 1 else
                              "HIP events on the compute stream around each step's gate")
-                            + (" (all chunks of this rank's shard)" if world > 1 else ""),
+                            + (" (all chunks of this rank's shard)" if sharded else ""),
                 **({"traffic_source": tsrc} if tsrc else {}),
             },
         }
-        if world == 1 and not a.no_cpu_baseline:
+        if not sharded and not a.no_cpu_baseline:
             result["cpu_baseline"] = cpu_baseline(host, n, L, a.cpu_seconds)
     if gate is not None:
         gate.close()
-    if world > 1:
+    if sharded:
         okt = torch.tensor([0 if ok else 1], dtype=torch.int32, device=dev)
         dist.broadcast(okt, src=0)
         ok = int(okt.item()) == 0

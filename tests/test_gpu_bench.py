@@ -1,0 +1,42 @@
+"""bench.py end to end on the GPU: the single-GPU line (config 2 path) and the N > 1 path rehearsed at
+one rank (--sharded: ufc_crc_sharded over RCCL, gather to rank 0, sampled oracle check).  Each run
+must print exactly one JSON line on stdout (the driver reads rank 0's stdout) and pass its own
+oracle checks."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, timeout=240):
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_single_gpu_line():
+    j = _run(["--steps", "5", "--warmup", "2", "--no-cpu-baseline", "--settle-ms", "5"])
+    assert j["n_gpus"] == 1 and j["config"]["global_frames"] == 1_000_000
+    assert "bit-exact vs the CPU oracle: True" in j["data"] and "valid flags as planted: True" in j["data"]
+    r = j["roofline"]
+    assert 0 < r["frac"] < 1 and r["kernel_avg_ms"] > 0 and j["ms_per_step"] > 0
+
+
+def test_bench_sharded_path_one_rank():
+    j = _run(["--sharded", "--global-frames", "5000000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
+              "--settle-ms", "5"])
+    assert j["scaling"] == "strong" and j["config"]["global_frames"] == 5_000_000
+    assert "bit-exact vs the oracle: True" in j["data"] and "valid flags as planted: True" in j["data"]
+    assert "ufc_crc_sharded" in j["roofline"]["kernel"]
