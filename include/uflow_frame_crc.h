@@ -35,7 +35,8 @@
  *     MI355X (gfx950) device ufc_ctx_create fails with UFC_ERR_NO_DEVICE.
  *   - One ufc_ctx per device.  Device launches on different streams of one context are safe while
  *     fewer than 64 are in flight (each takes a claim-counter slot); device scratch (batch parse,
- *     sorted varlen mode) is kept per stream.  The host-buffer calls (ufc_validate_host_*,
+ *     sorted varlen mode, the CRC words of a fixed seal called without d_crc_out) is kept per
+ *     stream and grows only on a stream's first or a larger batch.  The host-buffer calls (ufc_validate_host_*,
  *     ufc_seal_host_*) use the context's own streams and staging, one host thread at a time per
  *     context; they are synchronous and, on error too, return only once no copy touches the
  *     caller's buffers.  The scalar host functions are reentrant.
@@ -109,7 +110,8 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
 /* Frame i occupies d_bytes[d_offsets[i] .. d_offsets[i+1]) (CSR, n+1 offsets, nondecreasing). */
 int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
                          uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream);
-/* In-place seal of every frame (frame_len >= 4); d_crc_out nullable. */
+/* In-place seal of every frame (frame_len >= 4); d_crc_out nullable.  Fixed stride: two kernels
+ * (the CRC words, then every trailer with non-temporal stores; UFC_OPT_SEAL_KERNEL). */
 int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
                          uint32_t* d_crc_out, void* stream);
 int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
