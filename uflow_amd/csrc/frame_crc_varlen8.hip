@@ -39,6 +39,9 @@ constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the se
 constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
 constexpr int kV8Aux = 0;                  // default cache policy (shared boundary lines)
+constexpr uint32_t kNoSet = 0xFFFFFFFFu;   // a wave's set sequence past its last claimed run
+// The workgroup's run counter: nibble-image row 127, column 63 (columns 52..63 are never read).
+constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
 
 // Per-lane geometry of a set (one VGPR): pad [0,9), J [9,12), len >= 5 [12], t [13,15) (window
 // bytes past the frame), frame index in its run [16,22), past the batch end [22].
@@ -178,25 +181,54 @@ template <bool SEAL, bool PAIRS, int WAVES, int DEPTH>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
   constexpr int JM = kV8Blocks;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+#ifdef UFC_TUNING
+  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
   const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
   Lane8 L;
   init_lane8(L, lds, p.G);
   const uint64_t nfr = p.nframes;
   const uint32_t nruns = (uint32_t)((nfr + kRunFrames - 1) / kRunFrames);
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t W = gridDim.x * WAVES, w = blockIdx.x * WAVES + wid;
-  // This wave's sets: a contiguous range of runs (8 sets per run of 64 frames); k = 0 .. nk - 1
-  // is set setq(k) of the batch.  (Runs w, w + W, ... instead, every wave sweeping the batch
-  // together, measured the same.)
-  const uint32_t R0 = (uint32_t)((uint64_t)nruns * w / W), R1 = (uint32_t)((uint64_t)nruns * (w + 1) / W);
-  const uint32_t nk = (R1 - R0) * 8u;
-  auto setq = [&](uint32_t k) -> uint32_t { return R0 * 8u + k; };
+#ifdef UFC_TUNING
+  const uint32_t w = blockIdx.x * WAVES + wid;
+  uint32_t nk = 0;  // sets this wave computed (timeline dumps)
+#endif
+  // Schedule: the workgroup owns a contiguous range of runs [WR0, WR1) (8 sets per run of 64
+  // frames); wave i takes run WR0 + i first, then claims the next runs one at a time from a
+  // counter in LDS (ds_add_rtn: lgkmcnt, not the vmcnt queue of the loads).  With a static run
+  // range per wave, the 3 waves of a SIMD finished 400 us apart on config 3 (1200..1620 us: the
+  // oldest-first issue priority runs them at different speeds, and the last waves then ran alone
+  // with no latency hiding); claimed runs make a CU's waves finish within about one run.
+  const uint32_t WR0 = (uint32_t)((uint64_t)nruns * blockIdx.x / gridDim.x);
+  const uint32_t WR1 = (uint32_t)((uint64_t)nruns * (blockIdx.x + 1) / gridDim.x);
+  uint32_t* const ctr = (uint32_t*)(lds + kV8CtrAddr);
+  // The wave's set sequence: sets of run `run`, position `pos` next; kNoSet once the claims fail.
+  uint32_t run = WR0 + wid < WR1 ? WR0 + wid : kNoSet, pos = 0;
+  bool exhausted = run == kNoSet;
+  auto next_q = [&]() -> uint32_t {
+    if (pos == 8u) {
+      pos = 0;
+      if (!exhausted) {
+        uint32_t v = 0;
+        if (L.lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        v = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+        run = WR0 + v < WR1 ? WR0 + v : kNoSet;
+        exhausted = run == kNoSet;
+      } else {
+        run = kNoSet;
+      }
+    }
+    const uint32_t q = run == kNoSet ? kNoSet : run * 8u + pos;
+    pos++;
+    return q;
+  };
   const uint4* rec = (const uint4*)p.offsets;
   const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets_csr + nfr);
 
-  // This group's record of the wave's set k (the same 16 bytes in the group's 8 lanes).
-  auto load_rec = [&](uint32_t k) -> uint4 {
-    const uint32_t qc = nk ? setq(min(k, nk - 1u)) : 0u;  // (a wave without runs reads set 0)
+  // This group's record of set q (the same 16 bytes in the group's 8 lanes).
+  auto load_rec = [&](uint32_t q) -> uint4 {
+    const uint32_t qc = q == kNoSet ? 0u : q;  // (no set: reads set 0)
     const u32x4 r = *as_global<g_u32x4>((const uint32_t*)(rec + (uint64_t)qc * 8 + L.grp));
     return make_uint4(r.x, r.y, r.z, r.w);
   };
@@ -205,7 +237,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   // group-0 frame's start (CSR: the fast frames of a run lie within 64 x 1.5 KB of each other),
   // or the buffer itself for pairs over less than 2 GB (pairs may come in any order).
   const bool flat = PAIRS && p.frame_len < (1ull << 31) - (1ull << 20);
-  auto geometry = [&](uint32_t k, uint4 r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
+  auto geometry = [&](uint32_t q, uint4 r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const uint32_t len = min(r.z, 0x40000000u);  // (longer: J > 6, the byte path)
     const bool dead = (r.w >> 31) != 0;
@@ -230,7 +262,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     m.Jset = min(jmax, (uint32_t)JM);
     m.mixed = jmin != jmax;
     m.g1 = __builtin_amdgcn_ballot_w64(pad > 256u) != 0;
-    const bool live = k < nk && !m.slow;
+    const bool live = q != kNoSet && !m.slow;
     voff0 = live ? wrel + 16u * L.col : kV8Oob;
     return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | ((r.w & 63u) << 16) |
            ((dead ? 1u : 0u) << 22);
@@ -308,9 +340,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   };
 
   // Byte path of set q: any lengths, loads restricted to each frame; the same result handling.
-  auto slow_set = [&](uint32_t k) {
-    const uint4 r = load_rec(k);
-    const uint32_t q = setq(k);
+  auto slow_set = [&](uint32_t q) {
+    const uint4 r = load_rec(q);
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const bool dead = (r.w >> 31) != 0;
     const uint32_t len = dead ? 0u : r.z;
@@ -370,55 +401,84 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   static_assert(DEPTH == 2 || DEPTH == 3, "ring depth");
   Buf8<JM> B[DEPTH];
   uint4 O[DEPTH];
-  uint32_t GE[DEPTH], VO[DEPTH];
+  uint32_t GE[DEPTH], VO[DEPTH], QO[DEPTH], QG[DEPTH];  // set of O[i] / of GE[i], B[i]
   uint64_t SB[DEPTH];
   Set8Meta M[DEPTH];
-  uint32_t S = 0;  // the wave's set computed next
-  // prologue: records of S .. S + 2 DEPTH - 2, geometry + loads of S .. S + DEPTH - 2
+  // prologue: records of the wave's first 2 DEPTH - 1 sets, geometry + loads of the first
+  // DEPTH - 1 (all in the wave's first run, which needs no claim: 2 DEPTH - 1 <= 8)
   uint4 Rq[DEPTH];
+  uint32_t Qq[DEPTH];
 #pragma unroll
-  for (int i = 0; i < DEPTH; i++) Rq[i] = load_rec(S + i);
+  for (int i = 0; i < DEPTH; i++) {
+    Qq[i] = next_q();
+    Rq[i] = load_rec(Qq[i]);
+  }
 #pragma unroll
   for (int i = 0; i < DEPTH - 1; i++) {
-    GE[i] = geometry(S + i, Rq[i], VO[i], M[i], SB[i]);
+    QG[i] = Qq[i];
+    GE[i] = geometry(QG[i], Rq[i], VO[i], M[i], SB[i]);
     load_set(VO[i], GE[i], SB[i], B[i]);
-    O[i] = load_rec(S + DEPTH + i);
+    QO[i] = next_q();
+    O[i] = load_rec(QO[i]);
   }
   O[DEPTH - 1] = Rq[DEPTH - 1];
+  QO[DEPTH - 1] = Qq[DEPTH - 1];
   stage_store<WAVES * 64>(sr, lds);
   fixtab_store(lds, p.G);  // (then an LDS-only barrier, as in stage_store: the prefetches stay in flight)
+  // Runs WR0 .. WR0 + WAVES - 1 are taken statically.  (Set by the thread whose stage_store wrote
+  // the word, after it: program order, then the barrier below.)
+  if (threadIdx.x == 1023u % (WAVES * 64u)) *ctr = WAVES;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#ifdef UFC_TUNING
+  const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
+#endif
 
   // One step: geometry + loads of set S + DEPTH - 1 (record loaded DEPTH steps ago), the record of
   // set S + 2 DEPTH - 1, then compute set S.
   auto step = [&](int cs, int fs) {
-    GE[fs] = geometry(S + DEPTH - 1, O[fs], VO[fs], M[fs], SB[fs]);
+    QG[fs] = QO[fs];
+    GE[fs] = geometry(QG[fs], O[fs], VO[fs], M[fs], SB[fs]);
     load_set(VO[fs], GE[fs], SB[fs], B[fs]);
-    O[fs] = load_rec(S + 2 * DEPTH - 1);
+    QO[fs] = next_q();
+    O[fs] = load_rec(QO[fs]);
     __builtin_amdgcn_sched_barrier(0);
-    if (S < nk) {
+    if (QG[cs] != kNoSet) {
       if (!M[cs].slow)
-        compute(setq(S), GE[cs], M[cs], B[cs], VO[cs], SB[cs]);
+        compute(QG[cs], GE[cs], M[cs], B[cs], VO[cs], SB[cs]);
       else
-        slow_set(S);
+        slow_set(QG[cs]);
+#ifdef UFC_TUNING
+      nk++;
+#endif
     }
     __builtin_amdgcn_sched_barrier(0);
-    S++;
   };
+  // (a wave's sets are valid up to its first kNoSet, so a round stops at the first dead set)
   if constexpr (DEPTH == 3) {
-    while (S < nk) {
+    while (QG[0] != kNoSet) {
       step(0, 2);
       step(1, 0);
       step(2, 1);
     }
   } else {
-    while (S < nk) {
+    while (QG[0] != kNoSet) {
       step(0, 1);
       step(1, 0);
     }
   }
+#ifdef UFC_TUNING
+  if (p.dbg && L.lane == 0) {  // per-wave timeline (tools/wave_timeline.py)
+    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+    unsigned long long* d = p.dbg + 4 * w;
+    d[0] = t_start;
+    d[1] = t_staged;
+    d[2] = t_end;
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
+    d[3] = (unsigned long long)nk | ((unsigned long long)__smid() << 32) | ((unsigned long long)xcc << 56);
+  }
+#endif
 }
 
 #define UFC_V8_INST(SEAL, PAIRS, WV, D) \

@@ -354,9 +354,26 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
     uint64_t blocks = (nruns + waves - 1) / waves;
     if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
     if (blocks < 1) blocks = 1;
+#ifdef UFC_TUNING
+    const char* dbg_path = std::getenv("UFC_DBG_WAVES");  // per-wave timestamps (synchronous; tuning only)
+    unsigned long long* d_dbg = nullptr;
+    if (dbg_path && hipMalloc(&d_dbg, blocks * waves * 32) == hipSuccess) c.dbg = d_dbg;
+#endif
     void* args[] = {&c};
     e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
+#ifdef UFC_TUNING
+    if (d_dbg) {
+      std::vector<unsigned long long> h(blocks * waves * 4);
+      (void)hipStreamSynchronize(stream);
+      (void)hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost);
+      (void)hipFree(d_dbg);
+      if (FILE* f = std::fopen(dbg_path, "wb")) {
+        std::fwrite(h.data(), 8, h.size(), f);
+        std::fclose(f);
+      }
+    }
+#endif
   }
   return UFC_OK;
 }
