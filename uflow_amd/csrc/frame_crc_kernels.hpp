@@ -76,9 +76,11 @@ constexpr int kVarlen2Threads = 1024;
 const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // Sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): 8-frame sets from the
 // run-sorted records (p.offsets = records, p.offsets_csr = the CSR offsets or nullptr for pairs),
-// A^128 chain tables and the 32-slot nibble image.  waves/depth: 12/2 (product); others in tuning
-// builds.  Pairs need the buffer below 2^31 - 2^20 bytes (32-bit offsets from the buffer).
-const void* varlen8_kernel_symbol(bool seal, bool pairs, int waves, int depth);
+// A^128 chain tables and the 32-slot nibble image; 12 waves, 2 sets in flight per wave.  insort:
+// runs sorted inside the kernel from the CSR offsets / pairs in p.offsets (product); otherwise
+// p.offsets = sort_runs records (tuning builds only, A/B).  Pairs need the buffer below
+// 2^31 - 2^20 bytes (32-bit offsets from the buffer).
+const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort);
 // Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride
 // + lens[i] (ufc_validate_host_slots_async).
 int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream);

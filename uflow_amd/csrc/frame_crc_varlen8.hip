@@ -177,14 +177,13 @@ struct Buf8 {
 // WAVES waves per workgroup (one workgroup per CU); DEPTH sets per wave in the ring (the set
 // computed plus DEPTH - 1 in flight).  p.offsets = the run-sorted records, p.offsets_csr = the
 // CSR offsets (nullptr for pairs: p.frame_len = the buffer length, relative offsets < 2^31).
-template <bool SEAL, bool PAIRS, int WAVES, int DEPTH>
+template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
   constexpr int JM = kV8Blocks;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
 #ifdef UFC_TUNING
   const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-  const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
   Lane8 L;
   init_lane8(L, lds, p.G);
   const uint64_t nfr = p.nframes;
@@ -206,28 +205,91 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   // The wave's set sequence: sets of run `run`, position `pos` next; kNoSet once the claims fail.
   uint32_t run = WR0 + wid < WR1 ? WR0 + wid : kNoSet, pos = 0;
   bool exhausted = run == kNoSet;
+
+  // ---- INSORT: each run is ordered by block count inside the wave that takes it (replaces the
+  // sort_runs pre-pass and its 16-byte records).  Lane i reads frame i's offsets and the lanes'
+  // keys are ranked with ballots, as in sort_runs; the run's records then sit in lane = sorted
+  // position (SR, pushed with ds_permute) and a set's group takes its record with ds_bpermute.
+  // The next run is claimed, and its offsets loaded, one run ahead (raw_a / raw_b).
+  const uint64_t* offs = p.offsets;  // INSORT: CSR offsets (n + 1) or (start, end) pairs
+  struct SRec {
+    uint32_t a_lo, a_hi, len, info;
+  };
+  SRec SR{0u, 0u, 0u, 0x80000000u};
+  auto raw_load = [&](uint32_t r, uint64_t& a, uint64_t& b) {
+    const uint64_t f = (uint64_t)(r == kNoSet ? 0u : r) * kRunFrames + L.lane;
+    const uint64_t fi = f < nfr ? f : 0u;
+    a = *as_global<g_u64>(offs + (PAIRS ? 2 * fi : fi));
+    b = *as_global<g_u64>(offs + (PAIRS ? 2 * fi + 1 : fi + 1));
+  };
+  auto sort_run = [&](uint32_t r, uint64_t a, uint64_t b, SRec& out) {
+    const uint64_t f = (uint64_t)r * kRunFrames + L.lane;
+    const bool live = r != kNoSet && f < nfr;
+    const uint64_t len = (live && b >= a) ? b - a : 0u;
+    const uint64_t n4 = len >= 4 ? len - 4 : len;
+    const uint64_t J = (n4 + 8 + 255) >> 8;
+    const uint32_t key = !live ? 8u : ((len >= 4 && len < 0x40000000ull && J <= (uint64_t)JM) ? (uint32_t)J : 7u);
+    uint32_t below = 0, rank_in = 0;
+#pragma unroll
+    for (uint32_t k = 1; k <= 8; k++) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(key == k);
+      below += (k < key) ? (uint32_t)__builtin_popcountll(m) : 0u;
+      const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      rank_in = (k == key) ? rk : rank_in;
+    }
+    const int dst = (int)((below + rank_in) * 4u);
+    out.a_lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)a);
+    out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(a >> 32));
+    out.len = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)min(len, (uint64_t)0xFFFFFFFFu));
+    out.info = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(L.lane | (live ? 0u : 0x80000000u)));
+  };
+  auto take_rec = [&](const SRec& sr, uint32_t q) -> uint4 {
+    const int src = (int)(((q & 7u) * 8u + L.grp) * 4u);
+    return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_lo),
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_hi),
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.len),
+                      (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.info));
+  };
+  uint32_t run_nxt = kNoSet;
+  uint64_t raw_a = 0, raw_b = 0;
+  auto claim_next = [&]() {
+    run_nxt = kNoSet;
+    if (!exhausted) {
+      uint32_t v = 0;
+      if (L.lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      v = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+      if (WR0 + v < WR1) run_nxt = WR0 + v;
+      else exhausted = true;
+    }
+    if constexpr (INSORT) raw_load(run_nxt, raw_a, raw_b);
+  };
   auto next_q = [&]() -> uint32_t {
     if (pos == 8u) {
       pos = 0;
-      if (!exhausted) {
-        uint32_t v = 0;
-        if (L.lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        v = (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-        run = WR0 + v < WR1 ? WR0 + v : kNoSet;
-        exhausted = run == kNoSet;
+      if constexpr (INSORT) {
+        run = run_nxt;
+        sort_run(run, raw_a, raw_b, SR);
+        claim_next();
       } else {
-        run = kNoSet;
+        claim_next();
+        run = run_nxt;
       }
     }
     const uint32_t q = run == kNoSet ? kNoSet : run * 8u + pos;
     pos++;
     return q;
   };
+  // the wave's first run: offsets first (loads in flight while the tables' loads are issued)
+  uint64_t a0 = 0, b0 = 0;
+  if constexpr (INSORT) raw_load(run, a0, b0);
+  const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
+  if constexpr (INSORT) sort_run(run, a0, b0, SR);
   const uint4* rec = (const uint4*)p.offsets;
   const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets_csr + nfr);
 
   // This group's record of set q (the same 16 bytes in the group's 8 lanes).
   auto load_rec = [&](uint32_t q) -> uint4 {
+    if constexpr (INSORT) return take_rec(SR, q);
     const uint32_t qc = q == kNoSet ? 0u : q;  // (no set: reads set 0)
     const u32x4 r = *as_global<g_u32x4>((const uint32_t*)(rec + (uint64_t)qc * 8 + L.grp));
     return make_uint4(r.x, r.y, r.z, r.w);
@@ -341,7 +403,16 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 
   // Byte path of set q: any lengths, loads restricted to each frame; the same result handling.
   auto slow_set = [&](uint32_t q) {
-    const uint4 r = load_rec(q);
+    uint4 r;
+    if constexpr (INSORT) {  // (the run may have left SR: sort it again)
+      uint64_t a, b;
+      SRec T;
+      raw_load(q >> 3, a, b);
+      sort_run(q >> 3, a, b, T);
+      r = take_rec(T, q);
+    } else {
+      r = load_rec(q);
+    }
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const bool dead = (r.w >> 31) != 0;
     const uint32_t len = dead ? 0u : r.z;
@@ -434,6 +505,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 #ifdef UFC_TUNING
   const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
 #endif
+  if constexpr (INSORT) claim_next();  // the second run (the counter is set now)
 
   // One step: geometry + loads of set S + DEPTH - 1 (record loaded DEPTH steps ago), the record of
   // set S + 2 DEPTH - 1, then compute set S.
@@ -481,33 +553,34 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 #endif
 }
 
-#define UFC_V8_INST(SEAL, PAIRS, WV, D) \
-  template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, WV, D>(const KernelParams);
-// Product: 12 waves, 2 sets per wave in the ring (152-158 VGPRs: three waves per SIMD; config 3
-// 1.69 ms kernel against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill).
-UFC_V8_INST(false, false, 12, 2) UFC_V8_INST(true, false, 12, 2) UFC_V8_INST(false, true, 12, 2) UFC_V8_INST(true, true, 12, 2)
+#define UFC_V8_INST(SEAL, PAIRS, IS) \
+  template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, 12, 2, IS>(const KernelParams);
+// Product: 12 waves, 2 sets per wave in the ring (three waves per SIMD; config 3 1.69 ms kernel
+// against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill), runs sorted
+// in the kernel.  The pre-sorted variant (records from sort_runs) is kept for A/B in tuning builds.
+UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
 #ifdef UFC_TUNING
-UFC_V8_INST(false, false, 8, 3) UFC_V8_INST(false, false, 8, 2) UFC_V8_INST(false, false, 10, 2)
-UFC_V8_INST(false, false, 14, 2) UFC_V8_INST(false, false, 16, 2)
+UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
 #endif
 #undef UFC_V8_INST
 
-const void* varlen8_kernel_symbol(bool seal, bool pairs, int waves, int depth) {
-  if (waves == 12 && depth == 2) {
+const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort) {
+  if (insort) {
     if (pairs)
-      return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2>
-                  : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2>;
-    return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2>
-                : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2>;
+      return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true>
+                  : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, true>;
+    return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true>
+                : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true>;
   }
 #ifdef UFC_TUNING
-  if (!seal && !pairs && waves == 8 && depth == 3) return (const void*)frame_crc_varlen8_kernel<false, false, 8, 3>;
-  if (!seal && !pairs && waves == 8 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 8, 2>;
-  if (!seal && !pairs && waves == 10 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 10, 2>;
-  if (!seal && !pairs && waves == 14 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 14, 2>;
-  if (!seal && !pairs && waves == 16 && depth == 2) return (const void*)frame_crc_varlen8_kernel<false, false, 16, 2>;
-#endif
+  if (pairs)
+    return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, false>
+                : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, false>;
+  return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, false>
+              : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, false>;
+#else
   return nullptr;
+#endif
 }
 
 }  // namespace ufc_dev

@@ -318,17 +318,18 @@ int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   return UFC_OK;
 }
 
-// The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): run-sorted records
-// (ufc_dev::sort_runs) into per-stream scratch, then one launch per chunk of < 2^29 frames.  Any
+// The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): one launch per chunk of
+// < 2^29 frames, each run of 64 frames sorted by block count inside the kernel (tuning builds: the
+// sort_runs pre-pass into per-stream scratch instead, UFC_V8_PRESORT=1).  Any
 // buffer size: each set's loads are relative to the set's own base (a set whose frames lie
 // 2 GB or more apart, possible with pairs, runs on the kernel's byte path).
 int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  int waves = 12, depth = 2;
+  bool insort = true;  // runs sorted inside the kernel; UFC_V8_PRESORT=1 (tuning): the sort_runs pre-pass
 #ifdef UFC_TUNING
-  if (const char* wv = std::getenv("UFC_V8_WAVES")) waves = std::atoi(wv);
-  if (const char* dp = std::getenv("UFC_V8_DEPTH")) depth = std::atoi(dp);
+  if (const char* ps = std::getenv("UFC_V8_PRESORT")) insort = std::atoi(ps) == 0;
 #endif
-  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, waves, depth);
+  const int waves = 12;
+  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, insort);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain128;
   kp.nib_img = ctx->d_nib32;
@@ -337,16 +338,20 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   const uint64_t total = kp.nframes;
   hipError_t e;
   void* rec = nullptr;
-  const size_t need = (size_t)((std::min(chunk, total) + 63) / 64 * 64) * 16;
-  if ((e = stream_scratch(ctx, kScratchSortRec, stream, need, &rec)) != hipSuccess) return hip_fail(ctx, e);
+  if (!insort) {
+    const size_t need = (size_t)((std::min(chunk, total) + 63) / 64 * 64) * 16;
+    if ((e = stream_scratch(ctx, kScratchSortRec, stream, need, &rec)) != hipSuccess) return hip_fail(ctx, e);
+  }
   for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
     c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
-    if ((e = (hipError_t)ufc_dev::sort_runs(c.offsets, pairs, c.nframes, rec, stream)) != hipSuccess)
-      return hip_fail(ctx, e);
     c.offsets_csr = pairs ? nullptr : c.offsets;
-    c.offsets = (const uint64_t*)rec;
+    if (!insort) {
+      if ((e = (hipError_t)ufc_dev::sort_runs(c.offsets, pairs, c.nframes, rec, stream)) != hipSuccess)
+        return hip_fail(ctx, e);
+      c.offsets = (const uint64_t*)rec;
+    }
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
     // one workgroup per CU, at least one run of 64 frames per wave
