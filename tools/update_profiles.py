@@ -16,8 +16,7 @@ from pmc_summary import summarise  # noqa: E402
 BENCH_KERNEL = "fixed_kernel<6, false"
 # kernels of tools/bench_configs.py --only varlen,shard,seal,parse (name substrings)
 CFG_KERNELS = {
-    "varlen (config 3): 8-lane sorted-runs kernel": "frame_crc_varlen8_kernel<false, false",
-    "varlen (config 3): its sort pre-pass": "sort_runs_kernel<false>",
+    "varlen (config 3): 8-lane sorted-runs kernel (runs sorted in the kernel)": "frame_crc_varlen8_kernel<false, false",
     "seal (config 2 encode side), pass 2: non-temporal trailer stores": "seal_scatter_kernel",
     "validate, fixed 1500 B (config 2 in bench; config-4 shard and the seal's pass 1 in bench_configs)":
         "fixed_kernel<6, false",
