@@ -215,3 +215,37 @@ def test_parse_datagram_validity_flags(engine):
         k += int(infos[i]["item_count"])
     assert int(_host(used)[0]) == k
     assert counts[True] > 1000 and counts[False] > 1000, counts
+
+
+def test_varlen_claimed_runs_with_slow_sets(engine):
+    """Many runs per wave (claimed from the workgroup's LDS counter, each sorted inside the kernel)
+    with byte-path sets at every position of a run: 2M frames of 0..1700 B (frames over 1532 B,
+    under 4 B and empty frames take the byte path, which re-sorts its run), a partial last run,
+    every 101st frame flipped.  CSR, (start, end) pairs of the same frames in reverse order, and
+    the seal, each against the oracle."""
+    n = 2_000_003
+    rng = np.random.default_rng(0x5EED00C1)
+    lens = rng.integers(0, 1701, size=n).astype(np.uint64)
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    host = rng.integers(0, 256, size=int(off[-1]), dtype=np.uint8)
+    ref_sealed = host.copy()
+    oracle.seal_varlen_mt(ref_sealed, off, THREADS)  # frames < 4 B are left alone
+    d = torch.from_numpy(host).to(DEV)
+    offs = torch.from_numpy(off.view(np.int64)).to(DEV)
+    engine.seal_varlen(d, offs)
+    torch.cuda.synchronize()
+    assert torch.equal(d, torch.from_numpy(ref_sealed).to(DEV)), "seal differs from the oracle's"
+    live = np.nonzero(lens > 0)[0]
+    flipped = live[::101]
+    ref_sealed[off[flipped] + (lens[flipped] - 1) // 2] ^= 0x40
+    d = torch.from_numpy(ref_sealed).to(DEV)
+    ref_crc, ref_valid = oracle.validate_varlen_mt(ref_sealed, off, THREADS)
+    crc, valid = engine.crc_varlen(d, offs)
+    torch.cuda.synchronize()
+    _compare(crc, valid, ref_crc, ref_valid, "claimed runs, CSR")
+    rev = np.arange(n - 1, -1, -1)
+    pairs = np.stack([off[:-1][rev], off[1:][rev]], axis=1).astype(np.int64)
+    crc, valid = engine.crc_pairs(d, torch.from_numpy(pairs).to(DEV))
+    torch.cuda.synchronize()
+    _compare(crc, valid, ref_crc[rev], ref_valid[rev], "claimed runs, pairs")
