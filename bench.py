@@ -44,10 +44,10 @@ def parse():
                     help="strong scaling: frames of the whole batch (default: N > 1 -> 100M, config 4)")
     ap.add_argument("--frame-len", type=int, default=1500)
     ap.add_argument("--flip-every", type=int, default=1000)
-    ap.add_argument("--settle-ms", type=float, default=50.0,
+    ap.add_argument("--settle-ms", type=float, default=1000.0,
                     help="untimed back-to-back launches before the warmup steps: a GPU coming out of idle "
-                         "runs ~15%% slower for a few ms (DESIGN.md section 6); the timed steps measure the "
-                         "sustained rate")
+                         "runs slower at first, and the first process on a fresh box still ran 4%% slower "
+                         "after 50 ms (DESIGN.md section 6); the timed steps measure the sustained rate")
     ap.add_argument("--event-group", type=int, default=10,
                     help="HIP events around each group of k back-to-back timed gates (roofline.kernel_avg_ms = "
                          "group time / k; 1 = events around every gate, which adds ~6 us per step)")
