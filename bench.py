@@ -13,8 +13,11 @@ the CPU oracle (N = 1: every frame; N > 1: the valid flags of every frame and a 
 rank's CRC words on rank 0); a mismatch makes the run fail.
 
 Launch:  python bench.py [--gpus 1 --steps 50 --warmup 10]
+         python bench.py --gpus N ...   (N > 1: starts its N ranks itself with torch.distributed.run,
+                                         makes no GPU call, forwards rank 0's JSON line)
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
-Rank 0 prints one JSON line.
+Rank 0 prints one JSON line.  --one-device puts every rank on cuda:0 (RCCL told the ranks are on
+different hosts, NCCL_HOSTID, so it accepts them): a one-GPU rehearsal of the N > 1 send/recv path.
 """
 import argparse
 import json
@@ -54,6 +57,12 @@ def parse():
     ap.add_argument("--sharded", action="store_true",
                     help="take the N > 1 path (ufc_crc_sharded over RCCL, gather to rank 0, sampled oracle check) "
                          "even at N = 1: a one-GPU rehearsal of the driver's multi-GPU run")
+    ap.add_argument("--one-device", action="store_true",
+                    help="every rank on cuda:0 (one-GPU rehearsal of the N > 1 path: RCCL over its socket "
+                         "transport, each rank told it is on its own host via NCCL_HOSTID)")
+    ap.add_argument("--fake-worker", action="store_true",
+                    help="launcher test (CPU): each rank joins a gloo group and rank 0 prints the rank count")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the read-only streaming ceiling probe")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of each CPU baseline leg")
     return ap.parse_args()
@@ -154,8 +163,76 @@ def cpu_baseline(host, n, L, target_s):
     }
 
 
+def launch_ranks(a):
+    """--gpus N > 1 without a launcher: run N ranks of this script under torch.distributed.run as a
+    child process (this process makes no GPU call), forward rank 0's JSON line to stdout (other
+    output to stderr) and return the launcher's exit code (non-zero if any rank failed)."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print("bench: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=dict(os.environ))
+    lines = []
+    for line in p.stdout:
+        try:
+            j = json.loads(line)
+        except ValueError:
+            j = None
+        if isinstance(j, dict) and "metric" in j:
+            lines.append(line.strip())
+        else:
+            sys.stderr.write(line)
+            sys.stderr.flush()
+    rc = p.wait()
+    for line in lines:
+        print(line, flush=True)
+    if rc == 0 and len(lines) != 1:
+        print(f"bench: expected one JSON line from rank 0, got {len(lines)}", file=sys.stderr)
+        return 1
+    return rc
+
+
+def fake_worker(world, rank):
+    """The launcher's CPU test: no GPU, one gloo all-reduce over the ranks."""
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    print(f"rank {rank} of {world} alive", flush=True)  # non-JSON output is not forwarded as the line
+    if rank == 0:
+        print(json.dumps({"metric": "launcher test", "n_gpus": world, "ranks_seen": int(t.item()), "value": 0}),
+              flush=True)
+    dist.destroy_process_group()
+
+
+def read_ceiling(eng, buf, stream, groups=5, per_group=10):
+    """Plain read-only stream of buf (the gate's own frame buffer) timed like the gate: HIP events
+    around groups of back-to-back launches.  Returns (GB/s, ms per launch, bytes per launch)."""
+    sink = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    nbytes = eng.hbm_read_probe(buf, sink, stream=stream)
+    for _ in range(20):
+        eng.hbm_read_probe(buf, sink, stream=stream)
+    ts = []
+    for _ in range(groups):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(per_group):
+            eng.hbm_read_probe(buf, sink, stream=stream)
+        e1.record(stream)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) / per_group)
+    ms = float(np.mean(ts))
+    return nbytes / (ms * 1e-3) / 1e9, ms, nbytes
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -163,10 +240,19 @@ def main():
         print(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run "
               f"--nproc-per-node {a.gpus}", file=sys.stderr)
         sys.exit(2)
+    if a.fake_worker:
+        return fake_worker(world, rank)
     sharded = world > 1 or a.sharded
     if sharded and world == 1:  # a one-rank group without a launcher
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29531"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
+    if a.one_device:
+        # RCCL refuses two ranks on one GPU of one host; ranks on "different hosts" talk over its
+        # socket transport (loopback), which runs the same ncclSend/ncclRecv calls of ufc_crc_sharded.
+        local = 0
+        os.environ["NCCL_HOSTID"] = f"ufc-one-device-rank{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ.setdefault("NCCL_IB_DISABLE", "1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if sharded:
@@ -265,6 +351,11 @@ def main():
     kern_all = np.array([e0.elapsed_time(e1) / (g1 - g0) for (g0, g1), (e0, e1) in zip(groups, gev)])
     kern_ms = float(np.mean(kern_all))
 
+    # ---- read-only streaming ceiling, after the timed region, on rank 0 ----
+    ceiling = None
+    if rank == 0 and not a.no_ceiling:
+        ceiling = read_ceiling(eng, frames[: min(n, 1 << 22) * L], compute)
+
     # ---- correctness (after the timed region) ----
     import oracle
     crc, valid = slots[last]
@@ -344,8 +435,17 @@ def main():
                 **({"traffic_source": tsrc} if tsrc else {}),
             },
         }
-        if not sharded and not a.no_cpu_baseline:
-            result["cpu_baseline"] = cpu_baseline(host, n, L, a.cpu_seconds)
+        if ceiling is not None:
+            gbs, probe_ms, probe_bytes = ceiling
+            result["roofline"].update({
+                "ceiling_GBs": round(gbs, 1), "frac_of_ceiling": round(achieved / gbs, 4),
+                "ceiling_source": f"ufc_hbm_read_probe (hbm_probe.hip): a plain read-only stream of {probe_bytes} B "
+                                  f"of the same frame buffer, 16 B per lane, 4 KiB per wave in flight, 8 waves per "
+                                  f"CU; HIP events around 5 groups of 10 launches, {probe_ms:.4f} ms per launch"})
+        if not a.no_cpu_baseline:
+            if sharded:  # rank 0's own frames: a bounded sample of the same workload
+                host = frames[: min(n, 1_000_000) * L].cpu().numpy()
+            result["cpu_baseline"] = cpu_baseline(host, min(n, 1_000_000), L, a.cpu_seconds)
     if gate is not None:
         gate.close()
     if sharded:

@@ -122,6 +122,13 @@ int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offs
 int ufc_crc_batch_pairs(ufc_ctx* ctx, const uint8_t* d_bytes, size_t bytes_len, const uint64_t* d_pairs, size_t n,
                         uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream);
 
+/* Measurement context, not part of the CRC path: reads the first
+ * floor(bytes / 1024) KiB of d_buf as one plain contiguous stream (the access pattern an HBM read
+ * bandwidth ceiling is measured with) and XORs the data into *d_sink.  *bytes_read receives the byte
+ * count read.  bench.py times it beside the gate and reports roofline.ceiling_GBs. */
+int ufc_hbm_read_probe(ufc_ctx* ctx, const uint8_t* d_buf, size_t bytes, uint32_t* d_sink, size_t* bytes_read,
+                       void* stream);
+
 /* ---- host buffers in, host buffers out (the receive path of SURVEY.md config 5) ----
  * Copies the frames through pinned staging buffers owned by the context, runs the batched
  * gate on the device and copies crc/valid back; synchronous.  h_offsets as above. */
@@ -151,17 +158,49 @@ int ufc_seal_host_varlen(ufc_ctx* ctx, uint8_t* h_bytes, const uint64_t* h_offse
 /* ---- multi-GPU: one process per GPU, frames sharded by index, RCCL gather to a root ----
  * Replaces, for a batch spread over the GPUs of one node, the receive loop's per-datagram gate
  * (src/server/mod.rs:591-602 -> Frame::read, serial/mod.rs:675-690).  Rank r owns the frames
- * ufc_shard_range(n_total, nranks, r) = [n_total r / nranks, n_total (r+1) / nranks) of a batch of
- * n_total fixed-length frames; the only exchange is the per-frame CRC word and valid flag of every
- * frame, gathered into global frame order on the root over RCCL (xGMI point-to-point).  RCCL is
- * loaded at run time (librccl.so.1); without it these calls return UFC_ERR_COMM. */
+ * [bounds[r], bounds[r+1]) of a batch of n_total frames:
+ *   fixed length     ufc_shard_bounds_fixed: [n_total r / nranks, n_total (r+1) / nranks)
+ *   variable length  ufc_shard_bounds_varlen: split by bytes, a binary search of r * bytes / nranks
+ *                    in the batch's offsets.
+ * The only exchange is the per-frame CRC word and valid flag of every frame, gathered into global
+ * frame order on the root over RCCL (xGMI point-to-point).  RCCL is loaded at run time
+ * (librccl.so.1); without it the comm calls return UFC_ERR_COMM. */
 #define UFC_COMM_ID_BYTES 128
+#define UFC_MAX_RANKS 64
 typedef struct ufc_comm ufc_comm;
 int ufc_shard_range(uint64_t n_total, int nranks, int rank, uint64_t* first, uint64_t* count);
 /* The gather pipeline's chunk `chunk` of rank `rank`'s shard: global frames [*first, *first + *count).
  * Returns the number of chunks every shard of the batch is split into (1..16: one per <= 2^22 frames
  * of a shard), or UFC_ERR_INVALID_ARG. */
 int ufc_shard_chunk(uint64_t n_total, int nranks, int rank, int chunk, uint64_t* first, uint64_t* count);
+/* Shard boundaries, bounds[0 .. nranks] (bounds[0] = 0, bounds[nranks] = n_total, nondecreasing).
+ * _varlen: h_offsets[0 .. n_total] of the whole CSR batch (nondecreasing); bounds[r] = the first
+ * frame i with h_offsets[i] - h_offsets[0] >= r * B / nranks, B = h_offsets[n_total] - h_offsets[0]. */
+int ufc_shard_bounds_fixed(uint64_t n_total, int nranks, uint64_t* bounds);
+int ufc_shard_bounds_varlen(const uint64_t* h_offsets, uint64_t n_total, int nranks, uint64_t* bounds);
+/* The gather schedule, a pure function of (bounds, rank, root): the same on every rank, no device.
+ * Every shard is split into the same number of chunks K = ufc_shard_nchunks(bounds, nranks) (1..16,
+ * one per <= 2^22 frames of the largest shard); chunk c of a shard of `cnt` frames is its local frames
+ * [cnt c / K, cnt (c+1) / K).  Per chunk, in order, a rank performs its plan's operations:
+ *   UFC_OP_GATE  the batched gate over its local frames [src, src + count), results into its own
+ *                outputs at [dst, dst + count) (the root: global positions; others: shard-local)
+ *   UFC_OP_SEND  (non-root) its outputs [src, src + count) to `peer` (= root), landing at global dst
+ *   UFC_OP_RECV  (root) `peer`'s outputs [src, src + count) into its own outputs [dst, dst + count)
+ * All SEND/RECV of one chunk form one RCCL group.  Returns the number of operations of chunk `chunk`
+ * (writing at most max_ops of them; ops may be NULL to query), or UFC_ERR_INVALID_ARG. */
+#define UFC_OP_GATE 0
+#define UFC_OP_SEND 1
+#define UFC_OP_RECV 2
+typedef struct ufc_xfer {
+  int32_t op;
+  int32_t peer;
+  uint64_t src;
+  uint64_t dst;
+  uint64_t count;
+} ufc_xfer;
+int ufc_shard_nchunks(const uint64_t* bounds, int nranks);
+int ufc_shard_gather_plan(const uint64_t* bounds, int nranks, int rank, int root, int chunk, ufc_xfer* ops,
+                          int max_ops);
 /* On one rank: a fresh communicator id (ncclGetUniqueId), handed to every rank out of band. */
 int ufc_comm_id_create(uint8_t id[UFC_COMM_ID_BYTES]);
 /* Collective over the nranks processes (one per GPU, each with its own ufc_ctx). */
@@ -179,9 +218,20 @@ int ufc_comm_last_error(const ufc_comm* comm);
  *                output is complete once both streams are; a sender's output may be rewritten
  *                once gather_stream has passed this call.
  * One host thread per communicator at a time; every rank must make the same calls in the same
- * order with the same n_total, frame_len and root. */
+ * order with the same n_total, stride, frame_len, root and output nullness.  Arguments that every
+ * rank sees alike are checked before any transfer, so a bad call fails on every rank.  A failure
+ * that only this rank sees after the gather has begun (a HIP launch error) aborts the communicator
+ * (ncclCommAbort) and marks it unusable (later calls return UFC_ERR_COMM): the peers' transfers
+ * then fail or stall, and the caller must tear down every rank's communicator. */
 int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size_t frame_len, uint64_t n_total,
                     uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream);
+/* Variable-length form: rank r's shard is the frames [bounds[r], bounds[r+1]) (ufc_shard_bounds_varlen
+ * of the whole batch, the same array on every rank), given as a CSR batch of its own: frame k of the
+ * shard occupies d_bytes[d_offsets[k] .. d_offsets[k+1]), k < bounds[r+1] - bounds[r] (offsets relative
+ * to d_bytes, e.g. the batch's offsets minus the shard's first offset).  Outputs, streams and error
+ * behaviour as ufc_crc_sharded. */
+int ufc_crc_sharded_varlen(ufc_comm* comm, const uint8_t* d_bytes, const uint64_t* d_offsets, const uint64_t* bounds,
+                           uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream);
 
 #ifdef __cplusplus
 }

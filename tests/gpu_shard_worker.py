@@ -1,0 +1,103 @@
+"""One rank of tests/test_gpu_shard.py::test_ranks_on_one_device (run under torch.distributed.run).
+
+Every rank sits on cuda:0 of the one-GPU test box.  RCCL refuses two ranks on one device of one
+host, so each rank is told it is on a host of its own (NCCL_HOSTID) and RCCL connects them through
+its socket transport over loopback: the N > 1 branch of ufc_crc_sharded / ufc_crc_sharded_varlen --
+the ncclSend of every sender, the root's ncclRecv into global frame order, the chunk pipeline on a
+separate gather stream -- runs for real, only over a slower wire than xGMI.  The root checks every
+gathered CRC word and valid flag against the CPU oracle over the whole batch and prints one JSON line.
+"""
+import json
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+rank = int(os.environ["RANK"])
+world = int(os.environ["WORLD_SIZE"])
+os.environ["NCCL_HOSTID"] = f"ufc-test-rank{rank}"
+os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+os.environ.setdefault("NCCL_IB_DISABLE", "1")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import oracle  # noqa: E402
+from uflow_amd import synth  # noqa: E402
+from uflow_amd.batch import FrameCrcEngine  # noqa: E402
+from uflow_amd.shard import ShardedGate, comm_id_create, shard_bounds_fixed, shard_bounds_varlen  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    eng = FrameCrcEngine(0)
+    idt = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        idt.copy_(torch.frombuffer(bytearray(comm_id_create()), dtype=torch.uint8))
+    dist.broadcast(idt, src=0)
+    gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
+    gs = torch.cuda.Stream(dev)
+    result = {"world": world}
+
+    # ---- fixed length: 9,000,001 x 64 B, more than 2^22 frames per shard at world 2 (2 chunks) ----
+    total, L, root = 9_000_001, 64, world - 1
+    b = shard_bounds_fixed(total, world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+
+    def fixed_batch(first, n):
+        f = synth.fixed_frames(n, L, synth.SEED_CONFIG4, first_frame=first, device=dev)
+        eng.seal_fixed(f, L, n=n)
+        g0 = (first + 1012) // 1013 * 1013  # global frames 0, 1013, 2026, ... damaged
+        synth.flip_bits(f, torch.arange(g0 - first, n, 1013, device=dev) * L, byte_in_frame=L // 2)
+        return f
+
+    frames = fixed_batch(lo, hi - lo)
+    n_out = total if rank == root else hi - lo
+    crc = torch.full((n_out,), -1, dtype=torch.int32, device=dev)
+    valid = torch.full((n_out,), 7, dtype=torch.uint8, device=dev)
+    gate.crc_sharded(frames, L, total, crc, valid, root=root, gather_stream=gs)
+    torch.cuda.synchronize()
+    if rank == root:
+        host = fixed_batch(0, total).cpu().numpy()
+        ref_crc, ref_valid = oracle.validate_fixed_mt(host, L, L, total, 32)
+        result["fixed_crc_ok"] = bool(np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc))
+        result["fixed_valid_ok"] = bool(np.array_equal(valid.cpu().numpy(), ref_valid))
+        result["fixed_invalid"] = int(total - ref_valid.sum())
+    del frames
+
+    # ---- variable length: 1,500,001 x U[64, 1500] B, split by bytes, gathered to rank 0 ----
+    total, root = 1_500_001, 0
+    data, off = synth.varlen_batch(total, 64, 1500, synth.SEED_CONFIG3, device=dev)
+    eng.seal_varlen(data, off)
+    synth.flip_bits(data, off[:-1][::7], byte_in_frame=3)
+    h_off = off.cpu().numpy()
+    b = shard_bounds_varlen(h_off.view(np.uint64), world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    sdata = data[int(h_off[lo]):int(h_off[hi])].clone()  # this rank's bytes only
+    soff = (off[lo:hi + 1] - off[lo]).contiguous()
+    n_out = total if rank == root else hi - lo
+    crc = torch.full((n_out,), -1, dtype=torch.int32, device=dev)
+    valid = torch.full((n_out,), 7, dtype=torch.uint8, device=dev)
+    gate.crc_sharded_varlen(sdata, soff, b, crc, valid, root=root, gather_stream=gs)
+    torch.cuda.synchronize()
+    if rank == root:
+        ref_crc, ref_valid = oracle.validate_varlen_mt(data.cpu().numpy(), h_off.view(np.uint64), 32)
+        result["varlen_crc_ok"] = bool(np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc))
+        result["varlen_valid_ok"] = bool(np.array_equal(valid.cpu().numpy(), ref_valid))
+        result["varlen_invalid"] = int(total - ref_valid.sum())
+        result["varlen_bounds"] = [int(x) for x in b]
+
+    gate.close()
+    dist.barrier()
+    dist.destroy_process_group()
+    eng.close()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

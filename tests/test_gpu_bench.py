@@ -32,6 +32,7 @@ def test_bench_single_gpu_line():
     assert "bit-exact vs the CPU oracle: True" in j["data"] and "valid flags as planted: True" in j["data"]
     r = j["roofline"]
     assert 0 < r["frac"] < 1 and r["kernel_avg_ms"] > 0 and j["ms_per_step"] > 0
+    assert 0 < r["ceiling_GBs"] < 8000 and r["frac_of_ceiling"] > 0
 
 
 def test_bench_sharded_path_one_rank():
@@ -40,3 +41,14 @@ def test_bench_sharded_path_one_rank():
     assert j["scaling"] == "strong" and j["config"]["global_frames"] == 5_000_000
     assert "bit-exact vs the oracle: True" in j["data"] and "valid flags as planted: True" in j["data"]
     assert "ufc_crc_sharded" in j["roofline"]["kernel"]
+
+
+def test_bench_two_ranks_one_device():
+    """`bench.py --gpus 2` with no launcher: the bench starts its own two ranks; --one-device puts both
+    on cuda:0 (RCCL socket transport), so config 4's N > 1 path -- ufc_crc_sharded's sends and the
+    root's receives, two chunks per 5M-frame shard -- runs and is checked by bench's own oracle pass."""
+    j = _run(["--gpus", "2", "--one-device", "--global-frames", "10000000", "--steps", "3", "--warmup", "1",
+              "--settle-ms", "5", "--cpu-seconds", "0.5"], timeout=300)
+    assert j["n_gpus"] == 2 and j["scaling"] == "strong" and j["config"]["global_frames"] == 10_000_000
+    assert "bit-exact vs the oracle: True" in j["data"] and "valid flags as planted: True" in j["data"]
+    assert j["cpu_baseline"]["value"] > 0 and j["roofline"]["ceiling_GBs"] > 0

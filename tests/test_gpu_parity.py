@@ -507,6 +507,10 @@ def test_host_slots_async(engine):
             assert valid[i].item() == int(v) and (crc[i].item() & 0xFFFFFFFF) == c
     with pytest.raises(ValueError):  # device tensors are not host buffers
         engine.validate_host_slots_async(h_slots.cuda(), stride, h_lens, crc, valid, streams[0])
+    short = h_slots[:(len(h_lens) - 1) * stride + int(h_lens[-1]) - 1]  # ends inside the last datagram
+    if int(h_lens[-1]):
+        with pytest.raises(ValueError):
+            engine.validate_host_slots_async(short, stride, h_lens, crc, valid, streams[0])
     from uflow_amd import _native as N
     assert N.lib().ufc_validate_host_slots_async(engine._ctx, h_slots.data_ptr(), stride, h_lens.data_ptr(), 4,
                                                  crc.data_ptr(), valid.data_ptr(), None) == N.UFC_ERR_INVALID_ARG

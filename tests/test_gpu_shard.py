@@ -1,9 +1,19 @@
-"""GPU: the multi-GPU C ABI (ufc_comm_create + ufc_crc_sharded over RCCL) at world size 1 -- the one
-GPU of the test box.  The RCCL communicator is created through the library's own binding, the
-shard is gated chunk by chunk (front-readable chunks after the first), results land in their
-global positions, and every frame matches the oracle.  The point-to-point layout between ranks is
-covered on the CPU (tests/test_shard_gloo.py); N > 1 runs in the driver's 8-GPU bench.
+"""GPU: the multi-GPU C ABI (ufc_comm_create + ufc_crc_sharded / ufc_crc_sharded_varlen over RCCL).
+
+- World size 1 in this process: the RCCL communicator is created through the library's own
+  binding, the shard is gated chunk by chunk (front-readable chunks after the first), results land
+  in their global positions, and every frame matches the oracle.
+- World sizes 2 and 3 on the one GPU of the test box (tests/gpu_shard_worker.py under
+  torch.distributed.run): RCCL's socket transport stands in for xGMI, so the senders' ncclSend and
+  the root's ncclRecv into global frame order run for real; every gathered word is checked.
+The plan itself is checked in C (tests/c/c_abi_smoke.c) and executed over gloo (test_shard_gloo.py).
 """
+import json
+import os
+import socket
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 import torch
@@ -52,3 +62,49 @@ def test_sharded_rejects_bad_arguments(engine, gate):
         gate.crc_sharded(frames, 100, 10, crc, None, root=1)  # root outside the communicator
     with pytest.raises(ValueError):
         gate.crc_sharded(frames, 100, 11, crc, None)  # outputs shorter than the batch
+
+
+def test_sharded_varlen_world1_config3(engine, gate):
+    """ufc_crc_sharded_varlen at world size 1 on config 3's batch (10M x U[64,1500] B, 3 chunks):
+    every frame against the oracle."""
+    from uflow_amd.shard import shard_bounds_varlen
+    n = 10_000_000
+    data, off = synth.varlen_batch(n, 64, 1500, synth.SEED_CONFIG3, device=DEV)
+    engine.seal_varlen(data, off)
+    synth.flip_bits(data, off[:-1][::1001], byte_in_frame=5)
+    h_off = off.cpu().numpy().view(np.uint64)
+    b = shard_bounds_varlen(h_off, 1)
+    assert list(b) == [0, n]
+    crc = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    valid = torch.full((n,), 7, dtype=torch.uint8, device=DEV)
+    gate.crc_sharded_varlen(data, off, b, crc, valid, root=0, gather_stream=torch.cuda.Stream())
+    torch.cuda.synchronize()
+    ref_crc, ref_valid = oracle.validate_varlen_mt(data.cpu().numpy(), h_off, 64)
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc)
+    assert np.array_equal(valid.cpu().numpy(), ref_valid)
+    assert int(ref_valid.sum()) == n - len(range(0, n, 1001))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_on_one_device(world):
+    """The N > 1 send/recv branch of the C ABI, executed: `world` ranks on cuda:0, RCCL over its
+    socket transport (each rank on its own NCCL_HOSTID), fixed and variable-length batches gathered
+    to a root and checked frame by frame against the oracle (tests/gpu_shard_worker.py)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(repo, "tests", "gpu_shard_worker.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=repo)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    j = json.loads(lines[0])
+    assert j["world"] == world
+    assert j["fixed_crc_ok"] and j["fixed_valid_ok"] and j["fixed_invalid"] == len(range(0, 9_000_001, 1013))
+    assert j["varlen_crc_ok"] and j["varlen_valid_ok"] and j["varlen_invalid"] == len(range(0, 1_500_001, 7))
+    assert len(j["varlen_bounds"]) == world + 1 and 0 < j["varlen_bounds"][1] < 1_500_001

@@ -11,7 +11,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libuflowcrc.so")
-SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_crc_varlen2.hip", "frame_crc_varlen8.hip", "frame_parse.hip", "ufc_api.cpp", "ufc_shard.cpp", "crc_math.cpp",
+SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_crc_varlen2.hip", "frame_crc_varlen8.hip", "frame_parse.hip", "hbm_probe.hip", "ufc_api.cpp", "ufc_shard.cpp", "crc_math.cpp",
            "frame_codec.cpp"]
 HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp", "frame_codec_core.hpp", "frame_parse.hpp",
            "ufc_internal.hpp"]

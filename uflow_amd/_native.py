@@ -20,6 +20,8 @@ UFC_ERR_HIP = -3
 UFC_ERR_NOMEM = -4
 UFC_ERR_COMM = -5
 UFC_COMM_ID_BYTES = 128
+UFC_MAX_RANKS = 64
+UFC_OP_GATE, UFC_OP_SEND, UFC_OP_RECV = 0, 1, 2
 
 # ufc_ctx_set_option (include/uflow_frame_crc.h)
 UFC_OPT_FIXED_KERNEL, UFC_OPT_VARLEN_KERNEL, UFC_OPT_GENERIC_JC = 0, 1, 2
@@ -50,6 +52,8 @@ _SIGNATURES = {
                                             ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
     "ufc_seal_batch_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                              ctypes.c_void_p, ctypes.c_void_p]),
+    "ufc_hbm_read_probe": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_size_t), ctypes.c_void_p]),
     "ufc_validate_host_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                                 ctypes.c_void_p, ctypes.c_void_p]),
     "ufc_crc_batch_pairs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
@@ -66,6 +70,11 @@ _SIGNATURES = {
                                        ctypes.POINTER(ctypes.c_uint64)]),
     "ufc_shard_chunk": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "ufc_shard_bounds_fixed": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
+    "ufc_shard_bounds_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]),
+    "ufc_shard_nchunks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "ufc_shard_gather_plan": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                             ctypes.c_void_p, ctypes.c_int]),
     "ufc_comm_id_create": (ctypes.c_int, [ctypes.c_void_p]),
     "ufc_comm_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                        ctypes.c_void_p]),
@@ -73,6 +82,9 @@ _SIGNATURES = {
     "ufc_comm_last_error": (ctypes.c_int, [ctypes.c_void_p]),
     "ufc_crc_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "ufc_crc_sharded_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p]),
     # include/uflow_frame_codec.h
     "ufc_frame_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p,
                                       ctypes.c_size_t]),
@@ -115,6 +127,12 @@ class Item(ctypes.Structure):
 class Builder(ctypes.Structure):
     _fields_ = [("buf", ctypes.c_void_p), ("cap", ctypes.c_size_t), ("len", ctypes.c_size_t),
                 ("count", ctypes.c_uint32), ("kind", ctypes.c_uint32)]
+
+
+class Xfer(ctypes.Structure):
+    """ufc_xfer: one operation of the multi-GPU gather plan (ufc_shard_gather_plan)."""
+    _fields_ = [("op", ctypes.c_int32), ("peer", ctypes.c_int32), ("src", ctypes.c_uint64), ("dst", ctypes.c_uint64),
+                ("count", ctypes.c_uint64)]
 
 
 class DatagramRef(ctypes.Structure):

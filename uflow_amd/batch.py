@@ -141,6 +141,17 @@ class FrameCrcEngine:
                                         _ptr(valid_out), self._stream(stream)), "ufc_crc_batch_pairs")
         return crc_out, valid_out
 
+    # ---- measurement context (not the CRC path) ----
+    def hbm_read_probe(self, buf, sink, stream=None):
+        """ufc_hbm_read_probe: read buf (uint8, device) as one plain stream, XOR into sink (int32[1]);
+        returns the bytes read (whole KiB).  The bench's read-only streaming ceiling."""
+        self._check("buf", buf, (torch.uint8,), 0)
+        self._check("sink", sink, (torch.int32, torch.uint32), 1)
+        nread = ctypes.c_size_t()
+        check(lib().ufc_hbm_read_probe(self._ctx, _ptr(buf), buf.numel(), _ptr(sink), ctypes.byref(nread),
+                                       self._stream(stream)), "ufc_hbm_read_probe")
+        return nread.value
+
     # ---- Frame::read past the gate, on the device (uflow_frame_codec.h) ----
     def parse_varlen(self, data, offsets, valid, items_cap=None, stream=None):
         """Batched Frame::read of a CSR batch after the CRC gate (`valid`, from crc_varlen).
@@ -176,6 +187,8 @@ class FrameCrcEngine:
         slots = np.ascontiguousarray(slots, dtype=np.uint8)
         lens = np.ascontiguousarray(lens, dtype=np.uint32)
         n = lens.size
+        if n and slots.size < (n - 1) * slot_stride + int(lens[-1]):
+            raise ValueError("slots must hold slot n - 1 and its datagram")
         crc = np.empty(n, dtype=np.uint32)
         valid = np.empty(n, dtype=np.uint8)
         check(lib().ufc_validate_host_slots(self._ctx, slots.ctypes.data, slot_stride, lens.ctypes.data, n,
@@ -186,14 +199,18 @@ class FrameCrcEngine:
         """Queue the slots gate on `stream` (torch.cuda.Stream) and return at once: slots (uint8),
         lens (int32) and the outputs crc_out (int32[n]) / valid_out (uint8[n]) are host
         torch tensors, ideally pinned, that must stay alive and unmodified until the stream is done."""
-        n = lens.numel()
-        need = {"slots": (slots, torch.uint8, (n - 1) * slot_stride if n else 0), "lens": (lens, torch.int32, n),
-                "crc_out": (crc_out, torch.int32, n), "valid_out": (valid_out, torch.uint8, n)}
+        n = lens.numel() if isinstance(lens, torch.Tensor) else 0
+        need = {"lens": (lens, torch.int32, n), "crc_out": (crc_out, torch.int32, n),
+                "valid_out": (valid_out, torch.uint8, n), "slots": (slots, torch.uint8, 0)}
         for name, (t, dt, m) in need.items():
             if not isinstance(t, torch.Tensor) or t.is_cuda or not t.is_contiguous():
                 raise ValueError(f"{name} must be a contiguous host tensor")
             if t.dtype != dt or t.numel() < m:
                 raise ValueError(f"{name} must be {dt} with at least {m} elements")
+        # The copy reads (n - 1) * slot_stride + lens[n - 1] bytes of slots (ufc_api.cpp).
+        m = (n - 1) * slot_stride + int(lens[n - 1]) if n else 0
+        if slots.numel() < m:
+            raise ValueError(f"slots must hold at least {m} bytes (slot n - 1 and its datagram), got {slots.numel()}")
         check(lib().ufc_validate_host_slots_async(self._ctx, slots.data_ptr(), slot_stride, lens.data_ptr(), n,
                                                   crc_out.data_ptr(), valid_out.data_ptr(), stream.cuda_stream),
               "ufc_validate_host_slots_async")

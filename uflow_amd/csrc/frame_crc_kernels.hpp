@@ -88,6 +88,9 @@ int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t
 // every frame, non-temporal (frame_len >= 4).  Returns a hipError_t.
 int seal_scatter(uint8_t* bytes, uint64_t stride, uint64_t frame_len, uint64_t nframes, const uint32_t* crc,
                  void* stream);
+// Read-only streaming ceiling (hbm_probe.hip): the first nbytes / 1024 KB of bytes as one contiguous
+// stream, one workgroup of 8 waves per CU; XOR of the data into *sink.  Returns a hipError_t.
+int read_stream(const uint8_t* bytes, uint64_t nbytes, uint32_t* sink, int ncu, void* stream);
 // Claim-counter words per workgroup (the kernel uses the first two; one 128-byte line each).
 constexpr int kCtrWordsPerBlock = 32;
 

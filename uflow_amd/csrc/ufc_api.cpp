@@ -419,7 +419,7 @@ int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams
   return launch_lean_varlen(ctx, seal, kp, stream, pairs);
 }
 
-constexpr uint64_t kMaxFrameLen = (uint64_t)1 << 30;  // per-frame limit of the 32-bit offsets math
+using ufc_internal::kMaxFrameLen;
 
 }  // namespace
 
@@ -577,6 +577,15 @@ int ufc_ctx_destroy(ufc_ctx* ctx) {
   }
   delete ctx;
   return UFC_OK;
+}
+
+int ufc_hbm_read_probe(ufc_ctx* ctx, const uint8_t* d_buf, size_t bytes, uint32_t* d_sink, size_t* bytes_read,
+                       void* stream) {
+  if (!ctx || !d_sink || (bytes >= 1024 && !d_buf)) return UFC_ERR_INVALID_ARG;
+  if (bytes_read) *bytes_read = bytes / 1024 * 1024;
+  DeviceGuard g(ctx->device);
+  const hipError_t e = (hipError_t)ufc_dev::read_stream(d_buf, bytes, d_sink, ctx->ncu, stream);
+  return e == hipSuccess ? UFC_OK : hip_fail(ctx, e);
 }
 
 int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,

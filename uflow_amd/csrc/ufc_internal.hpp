@@ -10,6 +10,8 @@ struct ufc_ctx;
 
 namespace ufc_internal {
 
+constexpr uint64_t kMaxFrameLen = (uint64_t)1 << 30;  // per-frame limit of the 32-bit offsets math
+
 // ufc_crc_batch_fixed with front_ok: the bytes before d_frames are readable (a later part of a
 // larger batch), so the first frames need no edge handling.
 int crc_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame_len, size_t n, uint32_t* d_crc_out,

@@ -32,6 +32,7 @@ struct Rccl {
   ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
@@ -54,11 +55,13 @@ const Rccl& rccl() {
     r.GetUniqueId = (decltype(r.GetUniqueId))sym("ncclGetUniqueId");
     r.CommInitRank = (decltype(r.CommInitRank))sym("ncclCommInitRank");
     r.CommDestroy = (decltype(r.CommDestroy))sym("ncclCommDestroy");
+    r.CommAbort = (decltype(r.CommAbort))sym("ncclCommAbort");
     r.Send = (decltype(r.Send))sym("ncclSend");
     r.Recv = (decltype(r.Recv))sym("ncclRecv");
     r.GroupStart = (decltype(r.GroupStart))sym("ncclGroupStart");
     r.GroupEnd = (decltype(r.GroupEnd))sym("ncclGroupEnd");
-    r.ok = r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.Send && r.Recv && r.GroupStart && r.GroupEnd;
+    r.ok = r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.CommAbort && r.Send && r.Recv && r.GroupStart &&
+           r.GroupEnd;
   });
   return r;
 }
@@ -88,30 +91,161 @@ struct ufc_comm {
   int rank = 0;
   ncclComm_t nccl = nullptr;
   int last_nccl_error = 0;
+  bool broken = false;  // aborted after a rank-local failure mid-gather: every later call fails
   hipEvent_t ev[kMaxChunks] = {};
 };
 
 namespace {
 
+uint64_t mul_div(uint64_t a, uint64_t b, uint64_t c) { return (uint64_t)((unsigned __int128)a * b / c); }
+
 // Contiguous shard of `rank`: frames [n r / W, n (r + 1) / W) (sizes differ by at most one).
 void shard_of(uint64_t n, int nranks, int rank, uint64_t* first, uint64_t* count) {
-  const unsigned __int128 lo = (unsigned __int128)n * (unsigned)rank / (unsigned)nranks;
-  const unsigned __int128 hi = (unsigned __int128)n * (unsigned)(rank + 1) / (unsigned)nranks;
-  *first = (uint64_t)lo;
-  *count = (uint64_t)(hi - lo);
+  const uint64_t lo = mul_div(n, (unsigned)rank, (unsigned)nranks);
+  const uint64_t hi = mul_div(n, (unsigned)(rank + 1), (unsigned)nranks);
+  *first = lo;
+  *count = hi - lo;
 }
 
-// Chunks of a shard: the same function of (n_total, nranks) on every rank, so that the root knows
-// every sender's chunk sizes.  Chunk c of a shard of `count` frames: [count c / K, count (c+1) / K).
-int chunks_for(uint64_t n_total, int nranks) {
-  const uint64_t per = (n_total + nranks - 1) / nranks;
-  const uint64_t k = (per + (1ull << kChunkFramesLog2) - 1) >> kChunkFramesLog2;
+bool bounds_ok(const uint64_t* bounds, int nranks) {
+  if (!bounds || nranks < 1 || nranks > UFC_MAX_RANKS || bounds[0] != 0) return false;
+  for (int r = 0; r < nranks; r++)
+    if (bounds[r + 1] < bounds[r]) return false;
+  return true;
+}
+
+// Chunks per shard: the same function of the bounds on every rank, so that the root knows every
+// sender's chunk sizes.
+int nchunks_of(const uint64_t* bounds, int nranks) {
+  uint64_t per = 0;
+  for (int r = 0; r < nranks; r++) per = std::max(per, bounds[r + 1] - bounds[r]);
+  const uint64_t k = (per >> kChunkFramesLog2) + ((per & ((1ull << kChunkFramesLog2) - 1)) ? 1 : 0);
   return (int)std::max<uint64_t>(1, std::min<uint64_t>(kMaxChunks, k));
+}
+
+// The plan of one chunk (include/uflow_frame_crc.h, ufc_shard_gather_plan); returns the op count.
+int plan_chunk(const uint64_t* bounds, int nranks, int rank, int root, int K, int c, ufc_xfer* ops, int max_ops) {
+  int k = 0;
+  auto push = [&](int op, int peer, uint64_t src, uint64_t dst, uint64_t count) {
+    if (ops && k < max_ops) ops[k] = ufc_xfer{op, peer, src, dst, count};
+    k++;
+  };
+  const uint64_t cnt = bounds[rank + 1] - bounds[rank];
+  const uint64_t a = mul_div(cnt, (unsigned)c, (unsigned)K), b = mul_div(cnt, (unsigned)(c + 1), (unsigned)K);
+  const bool is_root = rank == root;
+  if (b > a) push(UFC_OP_GATE, rank, a, (is_root ? bounds[rank] : 0) + a, b - a);
+  if (nranks == 1) return k;
+  if (is_root) {
+    for (int p = 0; p < nranks; p++) {
+      if (p == root) continue;
+      const uint64_t pc = bounds[p + 1] - bounds[p];
+      const uint64_t pa = mul_div(pc, (unsigned)c, (unsigned)K), pb = mul_div(pc, (unsigned)(c + 1), (unsigned)K);
+      if (pb > pa) push(UFC_OP_RECV, p, pa, bounds[p] + pa, pb - pa);
+    }
+  } else if (b > a) {
+    push(UFC_OP_SEND, root, a, bounds[rank] + a, b - a);
+  }
+  return k;
 }
 
 int nccl_fail(ufc_comm* comm, ncclResult_t r) {
   comm->last_nccl_error = (int)r;
   return UFC_ERR_COMM;
+}
+
+// A failure only this rank sees, after the gather may have begun: abort the communicator so that no
+// later call queues transfers the peers cannot match.
+int abort_comm(ufc_comm* comm, int rc) {
+  if (comm->nccl && !comm->broken) (void)rccl().CommAbort(comm->nccl);
+  comm->nccl = nullptr;
+  comm->broken = true;
+  return rc;
+}
+
+// The gate of one chunk's frames, results into the rank's outputs at `dst`.
+using GateFn = int (*)(const void* args, uint64_t src, uint64_t count, uint32_t* crc, uint8_t* valid,
+                       hipStream_t s, bool front_ok);
+
+struct FixedArgs {
+  ufc_ctx* ctx;
+  const uint8_t* frames;
+  size_t stride, frame_len;
+};
+int gate_fixed(const void* p, uint64_t src, uint64_t count, uint32_t* crc, uint8_t* valid, hipStream_t s,
+               bool front_ok) {
+  const FixedArgs& a = *(const FixedArgs*)p;
+  return ufc_internal::crc_fixed(a.ctx, a.frames + src * a.stride, a.stride, a.frame_len, count, crc, valid, s,
+                                 front_ok);
+}
+
+struct VarlenArgs {
+  ufc_ctx* ctx;
+  const uint8_t* bytes;
+  const uint64_t* offsets;
+};
+int gate_varlen(const void* p, uint64_t src, uint64_t count, uint32_t* crc, uint8_t* valid, hipStream_t s, bool) {
+  const VarlenArgs& a = *(const VarlenArgs*)p;
+  return ufc_crc_batch_varlen(a.ctx, a.bytes, a.offsets + src, count, crc, valid, (void*)s);
+}
+
+// The chunked gate + gather of one rank, executing ufc_shard_gather_plan chunk by chunk.
+int run_sharded(ufc_comm* comm, const uint64_t* bounds, GateFn gate, const void* gargs, uint32_t* d_crc_out,
+                uint8_t* d_valid_out, int root, hipStream_t s, hipStream_t gs) {
+  const Rccl& r = rccl();
+  const int W = comm->nranks;
+  const int K = nchunks_of(bounds, W);
+  DeviceGuard g(ufc_internal::ctx_device(comm->ctx));
+  ufc_xfer ops[UFC_MAX_RANKS + 1];
+  for (int c = 0; c < K; c++) {
+    const int nops = plan_chunk(bounds, W, comm->rank, root, K, c, ops, UFC_MAX_RANKS + 1);
+    bool xfer = false;
+    for (int i = 0; i < nops; i++) {
+      const ufc_xfer& o = ops[i];
+      if (o.op != UFC_OP_GATE) {
+        xfer = true;
+        continue;
+      }
+      const int rc = gate(gargs, o.src, o.count, d_crc_out ? d_crc_out + o.dst : nullptr,
+                          d_valid_out ? d_valid_out + o.dst : nullptr, s, c > 0);
+      if (rc != UFC_OK) return W > 1 ? abort_comm(comm, rc) : rc;
+    }
+    if (!xfer) continue;  // (one rank, or nothing of this chunk to move)
+    if (gs != s) {
+      hipError_t e = hipEventRecord(comm->ev[c], s);
+      if (e == hipSuccess) e = hipStreamWaitEvent(gs, comm->ev[c], 0);
+      if (e != hipSuccess) {
+        ufc_internal::note_hip_error(comm->ctx, (int)e);
+        return abort_comm(comm, UFC_ERR_HIP);
+      }
+    }
+    ncclResult_t nr = r.GroupStart();
+    if (nr != ncclSuccess) return abort_comm(comm, nccl_fail(comm, nr));
+    for (int i = 0; i < nops && nr == ncclSuccess; i++) {
+      const ufc_xfer& o = ops[i];
+      if (o.op == UFC_OP_SEND) {
+        if (d_crc_out) nr = r.Send(d_crc_out + o.src, o.count, ncclUint32, o.peer, comm->nccl, gs);
+        if (nr == ncclSuccess && d_valid_out)
+          nr = r.Send(d_valid_out + o.src, o.count, ncclUint8, o.peer, comm->nccl, gs);
+      } else if (o.op == UFC_OP_RECV) {
+        if (d_crc_out) nr = r.Recv(d_crc_out + o.dst, o.count, ncclUint32, o.peer, comm->nccl, gs);
+        if (nr == ncclSuccess && d_valid_out)
+          nr = r.Recv(d_valid_out + o.dst, o.count, ncclUint8, o.peer, comm->nccl, gs);
+      }
+    }
+    const ncclResult_t ne = r.GroupEnd();
+    if (nr != ncclSuccess) return abort_comm(comm, nccl_fail(comm, nr));
+    if (ne != ncclSuccess) return abort_comm(comm, nccl_fail(comm, ne));
+  }
+  return UFC_OK;
+}
+
+// Checks every rank makes alike (same arguments on every rank by contract): a failure here happens
+// on every rank before any transfer.
+int check_common(ufc_comm* comm, int root, bool any_out) {
+  if (!comm) return UFC_ERR_INVALID_ARG;
+  if (comm->broken) return UFC_ERR_COMM;
+  if (root < 0 || root >= comm->nranks || !any_out) return UFC_ERR_INVALID_ARG;
+  return UFC_OK;
 }
 
 }  // namespace
@@ -124,14 +258,54 @@ int ufc_shard_range(uint64_t n_total, int nranks, int rank, uint64_t* first, uin
   return UFC_OK;
 }
 
-int ufc_shard_chunk(uint64_t n_total, int nranks, int rank, int chunk, uint64_t* first, uint64_t* count) {
-  if (nranks < 1 || rank < 0 || rank >= nranks || !first || !count) return UFC_ERR_INVALID_ARG;
-  const int K = chunks_for(n_total, nranks);
+int ufc_shard_bounds_fixed(uint64_t n_total, int nranks, uint64_t* bounds) {
+  if (!bounds || nranks < 1 || nranks > UFC_MAX_RANKS) return UFC_ERR_INVALID_ARG;
+  for (int r = 0; r <= nranks; r++) bounds[r] = mul_div(n_total, (unsigned)r, (unsigned)nranks);
+  return UFC_OK;
+}
+
+int ufc_shard_bounds_varlen(const uint64_t* h_offsets, uint64_t n_total, int nranks, uint64_t* bounds) {
+  if (!h_offsets || !bounds || nranks < 1 || nranks > UFC_MAX_RANKS) return UFC_ERR_INVALID_ARG;
+  const uint64_t base = h_offsets[0];
+  if (h_offsets[n_total] < base) return UFC_ERR_INVALID_ARG;
+  const uint64_t B = h_offsets[n_total] - base;
+  bounds[0] = 0;
+  bounds[nranks] = n_total;
+  for (int r = 1; r < nranks; r++) {
+    // First frame starting at or past byte r B / W of the batch (lower_bound over offsets[0..n]).
+    const uint64_t target = base + mul_div(B, (unsigned)r, (unsigned)nranks);
+    const uint64_t* it = std::lower_bound(h_offsets, h_offsets + n_total + 1, target);
+    bounds[r] = std::min<uint64_t>((uint64_t)(it - h_offsets), n_total);
+    if (bounds[r] < bounds[r - 1]) return UFC_ERR_INVALID_ARG;  // offsets not sorted
+  }
+  return UFC_OK;
+}
+
+int ufc_shard_nchunks(const uint64_t* bounds, int nranks) {
+  if (!bounds_ok(bounds, nranks)) return UFC_ERR_INVALID_ARG;
+  return nchunks_of(bounds, nranks);
+}
+
+int ufc_shard_gather_plan(const uint64_t* bounds, int nranks, int rank, int root, int chunk, ufc_xfer* ops,
+                          int max_ops) {
+  if (!bounds_ok(bounds, nranks) || rank < 0 || rank >= nranks || root < 0 || root >= nranks || max_ops < 0 ||
+      (max_ops > 0 && !ops))
+    return UFC_ERR_INVALID_ARG;
+  const int K = nchunks_of(bounds, nranks);
   if (chunk < 0 || chunk >= K) return UFC_ERR_INVALID_ARG;
-  uint64_t lo, cnt;
-  shard_of(n_total, nranks, rank, &lo, &cnt);
-  const uint64_t a = cnt * (uint64_t)chunk / K, b = cnt * (uint64_t)(chunk + 1) / K;
-  *first = lo + a;
+  return plan_chunk(bounds, nranks, rank, root, K, chunk, ops, max_ops);
+}
+
+int ufc_shard_chunk(uint64_t n_total, int nranks, int rank, int chunk, uint64_t* first, uint64_t* count) {
+  if (nranks < 1 || nranks > UFC_MAX_RANKS || rank < 0 || rank >= nranks || !first || !count)
+    return UFC_ERR_INVALID_ARG;
+  uint64_t bounds[UFC_MAX_RANKS + 1];
+  (void)ufc_shard_bounds_fixed(n_total, nranks, bounds);
+  const int K = nchunks_of(bounds, nranks);
+  if (chunk < 0 || chunk >= K) return UFC_ERR_INVALID_ARG;
+  const uint64_t cnt = bounds[rank + 1] - bounds[rank];
+  const uint64_t a = mul_div(cnt, (unsigned)chunk, (unsigned)K), b = mul_div(cnt, (unsigned)(chunk + 1), (unsigned)K);
+  *first = bounds[rank] + a;
   *count = b - a;
   return K;
 }
@@ -150,7 +324,7 @@ int ufc_comm_id_create(uint8_t id[UFC_COMM_ID_BYTES]) {
 int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const uint8_t id[UFC_COMM_ID_BYTES]) {
   if (!out) return UFC_ERR_INVALID_ARG;
   *out = nullptr;
-  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return UFC_ERR_INVALID_ARG;
+  if (!ctx || !id || nranks < 1 || nranks > UFC_MAX_RANKS || rank < 0 || rank >= nranks) return UFC_ERR_INVALID_ARG;
   const Rccl& r = rccl();
   if (!r.ok) return UFC_ERR_COMM;
   ufc_comm* c = new (std::nothrow) ufc_comm();
@@ -195,62 +369,31 @@ int ufc_comm_last_error(const ufc_comm* comm) { return comm ? comm->last_nccl_er
 
 int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size_t frame_len, uint64_t n_total,
                     uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream) {
-  if (!comm) return UFC_ERR_INVALID_ARG;
-  if (root < 0 || root >= comm->nranks || stride < frame_len || (!d_crc_out && !d_valid_out))
-    return UFC_ERR_INVALID_ARG;
-  uint64_t lo, cnt;
-  shard_of(n_total, comm->nranks, comm->rank, &lo, &cnt);
-  if (cnt && !d_frames) return UFC_ERR_INVALID_ARG;
-  const Rccl& r = rccl();
+  if (const int rc = check_common(comm, root, d_crc_out || d_valid_out)) return rc;
+  if (stride < frame_len || frame_len > ufc_internal::kMaxFrameLen) return UFC_ERR_INVALID_ARG;
+  uint64_t bounds[UFC_MAX_RANKS + 1];
+  (void)ufc_shard_bounds_fixed(n_total, comm->nranks, bounds);
+  const uint64_t cnt = bounds[comm->rank + 1] - bounds[comm->rank];
+  // Rank-local: this rank's frames.  Fails before any transfer here, but the peers' transfers to or
+  // from this rank then stall: abort, so the failure is visible (ufc_comm_last_error / broken).
+  if (cnt && !d_frames) return comm->nranks > 1 ? abort_comm(comm, UFC_ERR_INVALID_ARG) : UFC_ERR_INVALID_ARG;
+  const FixedArgs args{comm->ctx, d_frames, stride, frame_len};
   hipStream_t s = (hipStream_t)stream;
-  hipStream_t gs = gather_stream ? (hipStream_t)gather_stream : s;
-  const bool is_root = comm->rank == root;
-  DeviceGuard g(ufc_internal::ctx_device(comm->ctx));
-  const int K = chunks_for(n_total, comm->nranks);
-  // This rank's results: on the root straight into their global position, elsewhere at the start
-  // of the caller's (shard-sized) output.
-  uint32_t* my_crc = d_crc_out ? d_crc_out + (is_root ? lo : 0) : nullptr;
-  uint8_t* my_valid = d_valid_out ? d_valid_out + (is_root ? lo : 0) : nullptr;
-  for (int c = 0; c < K; c++) {
-    const uint64_t a = cnt * (uint64_t)c / K, b = cnt * (uint64_t)(c + 1) / K;
-    if (b > a) {
-      const int rc = ufc_internal::crc_fixed(comm->ctx, d_frames + a * stride, stride, frame_len, b - a,
-                                             my_crc ? my_crc + a : nullptr, my_valid ? my_valid + a : nullptr, s,
-                                             c > 0);
-      if (rc != UFC_OK) return rc;
-    }
-    if (comm->nranks == 1) continue;
-    if (gs != s) {
-      hipError_t e = hipEventRecord(comm->ev[c], s);
-      if (e == hipSuccess) e = hipStreamWaitEvent(gs, comm->ev[c], 0);
-      if (e != hipSuccess) {
-        ufc_internal::note_hip_error(comm->ctx, (int)e);
-        return UFC_ERR_HIP;
-      }
-    }
-    ncclResult_t nr = r.GroupStart();
-    if (nr != ncclSuccess) return nccl_fail(comm, nr);
-    if (is_root) {
-      for (int p = 0; p < comm->nranks; p++) {
-        if (p == root) continue;
-        uint64_t plo, pcnt;
-        shard_of(n_total, comm->nranks, p, &plo, &pcnt);
-        const uint64_t pa = pcnt * (uint64_t)c / K, pb = pcnt * (uint64_t)(c + 1) / K;
-        if (pb == pa) continue;
-        if (d_crc_out && (nr = r.Recv(d_crc_out + plo + pa, pb - pa, ncclUint32, p, comm->nccl, gs)) != ncclSuccess)
-          break;
-        if (d_valid_out && (nr = r.Recv(d_valid_out + plo + pa, pb - pa, ncclUint8, p, comm->nccl, gs)) != ncclSuccess)
-          break;
-      }
-    } else if (b > a) {
-      if (my_crc) nr = r.Send(my_crc + a, b - a, ncclUint32, root, comm->nccl, gs);
-      if (nr == ncclSuccess && my_valid) nr = r.Send(my_valid + a, b - a, ncclUint8, root, comm->nccl, gs);
-    }
-    const ncclResult_t ne = r.GroupEnd();
-    if (nr != ncclSuccess) return nccl_fail(comm, nr);
-    if (ne != ncclSuccess) return nccl_fail(comm, ne);
-  }
-  return UFC_OK;
+  return run_sharded(comm, bounds, gate_fixed, &args, d_crc_out, d_valid_out, root, s,
+                     gather_stream ? (hipStream_t)gather_stream : s);
+}
+
+int ufc_crc_sharded_varlen(ufc_comm* comm, const uint8_t* d_bytes, const uint64_t* d_offsets, const uint64_t* bounds,
+                           uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream) {
+  if (const int rc = check_common(comm, root, d_crc_out || d_valid_out)) return rc;
+  if (!bounds_ok(bounds, comm->nranks)) return UFC_ERR_INVALID_ARG;
+  const uint64_t cnt = bounds[comm->rank + 1] - bounds[comm->rank];
+  if (cnt && (!d_bytes || !d_offsets))
+    return comm->nranks > 1 ? abort_comm(comm, UFC_ERR_INVALID_ARG) : UFC_ERR_INVALID_ARG;
+  const VarlenArgs args{comm->ctx, d_bytes, d_offsets};
+  hipStream_t s = (hipStream_t)stream;
+  return run_sharded(comm, bounds, gate_varlen, &args, d_crc_out, d_valid_out, root, s,
+                     gather_stream ? (hipStream_t)gather_stream : s);
 }
 
 }  // extern "C"

@@ -7,9 +7,12 @@ There is no data-path collective: every rank validates its own contiguous frame 
 """
 import ctypes
 
+import numpy as np
 import torch
 
-from ._native import UFC_COMM_ID_BYTES, check, lib
+from ._native import UFC_COMM_ID_BYTES, UFC_MAX_RANKS, Xfer, check, lib
+
+OP_GATE, OP_SEND, OP_RECV = 0, 1, 2
 
 
 def shard_range(total, rank, world):
@@ -35,6 +38,50 @@ def shard_chunks(total, rank, world):
             check(rc, "ufc_shard_chunk")
         out.append((first.value, first.value + count.value))
     return out
+
+
+def _bounds_arg(bounds):
+    b = np.ascontiguousarray(bounds, dtype=np.uint64)
+    return b, b.ctypes.data_as(ctypes.c_void_p)
+
+
+def shard_bounds_fixed(total, world):
+    """ufc_shard_bounds_fixed: rank r owns frames [b[r], b[r+1])."""
+    if not 1 <= world <= UFC_MAX_RANKS:
+        raise ValueError("bad world size")
+    b = np.zeros(world + 1, np.uint64)
+    check(lib().ufc_shard_bounds_fixed(total, world, b.ctypes.data_as(ctypes.c_void_p)), "ufc_shard_bounds_fixed")
+    return b
+
+
+def shard_bounds_varlen(offsets, world):
+    """ufc_shard_bounds_varlen: the batch split by bytes (binary search of r * bytes / world in the
+    CSR offsets, n + 1 entries)."""
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    if off.ndim != 1 or off.size < 1 or not 1 <= world <= UFC_MAX_RANKS:
+        raise ValueError("offsets must be a 1-D array of n + 1 entries; 1 <= world <= 64")
+    b = np.zeros(world + 1, np.uint64)
+    check(lib().ufc_shard_bounds_varlen(off.ctypes.data_as(ctypes.c_void_p), off.size - 1, world,
+                                        b.ctypes.data_as(ctypes.c_void_p)), "ufc_shard_bounds_varlen")
+    return b
+
+
+def gather_plan(bounds, rank, root):
+    """The C gather schedule (ufc_shard_nchunks + ufc_shard_gather_plan) of `rank`: one list of
+    (op, peer, src, dst, count) per chunk, executed in order (SEND/RECV of a chunk grouped)."""
+    b, bp = _bounds_arg(bounds)
+    world = b.size - 1
+    k = lib().ufc_shard_nchunks(bp, world)
+    if k < 0:
+        check(k, "ufc_shard_nchunks")
+    ops = (Xfer * (UFC_MAX_RANKS + 1))()
+    plan = []
+    for c in range(k):
+        m = lib().ufc_shard_gather_plan(bp, world, rank, root, c, ops, len(ops))
+        if m < 0:
+            check(m, "ufc_shard_gather_plan")
+        plan.append([(o.op, o.peer, o.src, o.dst, o.count) for o in ops[:m]])
+    return plan
 
 
 def comm_id_create():
@@ -86,3 +133,22 @@ class ShardedGate:
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         check(lib().ufc_crc_sharded(self._comm, p(frames), stride, frame_len, n_total, p(crc_out), p(valid_out), root,
                                     s, gs), "ufc_crc_sharded")
+
+    def crc_sharded_varlen(self, data, offsets, bounds, crc_out, valid_out, root=0, stream=None, gather_stream=None):
+        """data / offsets: this rank's shard as a CSR batch of its own (offsets int64 on the device,
+        bounds[r+1] - bounds[r] + 1 entries, relative to data).  bounds: shard_bounds_varlen of the
+        whole batch, the same on every rank.  Outputs as crc_sharded."""
+        b, bp = _bounds_arg(bounds)
+        if b.size != self.world + 1:
+            raise ValueError("bounds must have world + 1 entries")
+        lo, hi = int(b[self.rank]), int(b[self.rank + 1])
+        n_out = int(b[-1]) if self.rank == root else hi - lo
+        eng = self.engine
+        eng._check("offsets", offsets, (torch.int64,), hi - lo + 1)
+        eng._check("data", data, (torch.uint8,), 0)
+        eng._check_outputs(n_out, crc_out, valid_out)
+        s = eng._stream(stream)
+        gs = eng._stream(gather_stream) if gather_stream is not None else None
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        check(lib().ufc_crc_sharded_varlen(self._comm, p(data), p(offsets), bp, p(crc_out), p(valid_out), root, s, gs),
+              "ufc_crc_sharded_varlen")
