@@ -5,7 +5,7 @@ host, so each rank is told it is on a host of its own (NCCL_HOSTID) and RCCL con
 its socket transport over loopback: the N > 1 branch of ufc_crc_sharded / ufc_crc_sharded_varlen --
 the ncclSend of every sender, the root's ncclRecv into global frame order, the chunk pipeline on a
 separate gather stream -- runs for real, only over a slower wire than xGMI.  The root checks every
-gathered CRC word and valid flag against the CPU oracle over the whole batch and prints one JSON line.
+gathered CRC word and valid flag against the CPU oracle over the whole batch and prints one JSON line (the fixed batch's root is the last rank, the variable-length batch's rank 0).
 """
 import json
 import os
@@ -41,7 +41,7 @@ def main():
     dist.broadcast(idt, src=0)
     gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
     gs = torch.cuda.Stream(dev)
-    result = {"world": world}
+    result = {"world": world, "rank": rank}
 
     # ---- fixed length: 9,000,001 x 64 B, more than 2^22 frames per shard at world 2 (2 chunks) ----
     total, L, root = 9_000_001, 64, world - 1
@@ -95,7 +95,7 @@ def main():
     dist.barrier()
     dist.destroy_process_group()
     eng.close()
-    if rank == 0:
+    if len(result) > 2:  # the roots of the two gathers print what they checked
         print(json.dumps(result), flush=True)
 
 

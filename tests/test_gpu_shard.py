@@ -102,8 +102,10 @@ def test_ranks_on_one_device(world):
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=repo)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, p.stdout[-2000:]
-    j = json.loads(lines[0])
+    assert len(lines) == 2, p.stdout[-2000:]  # one line per root (last rank: fixed; rank 0: varlen)
+    j = {}
+    for ln in lines:
+        j.update(json.loads(ln))
     assert j["world"] == world
     assert j["fixed_crc_ok"] and j["fixed_valid_ok"] and j["fixed_invalid"] == len(range(0, 9_000_001, 1013))
     assert j["varlen_crc_ok"] and j["varlen_valid_ok"] and j["varlen_invalid"] == len(range(0, 1_500_001, 7))
