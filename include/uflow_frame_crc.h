@@ -81,18 +81,20 @@ const char* ufc_error_string(int code);
 int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 
 /* Kernel-selection options of a context (A/B measurement and tests; the defaults are the measured
- * fastest).  Results never depend on them.  Set between calls, not while work is queued. */
+ * fastest).  Results never depend on them.  Set between calls, not while work is queued.  Values
+ * marked (tuning) select kernels measured slower than the default; they exist only in -DUFC_TUNING
+ * builds of the library, and ufc_ctx_set_option rejects them (UFC_ERR_INVALID_ARG) in the product. */
 #define UFC_OPT_FIXED_KERNEL 0   /* fixed-stride batches: */
 #define UFC_FIXED_AUTO 0         /*   lean kernel when eligible (default) */
 #define UFC_FIXED_GENERIC 1      /*   the generic kernel */
-#define UFC_FIXED_CLAIM16 2      /*   lean kernel, claimed schedule at 16 waves (round-1 default) */
+#define UFC_FIXED_CLAIM16 2      /*   (tuning) lean kernel, claimed schedule at 16 waves (round-1 default) */
 #define UFC_OPT_VARLEN_KERNEL 1  /* CSR / pairs batches: */
-#define UFC_VARLEN_AUTO 0        /*   the default: UFC_VARLEN_SORTED8 (else UFC_VARLEN_SORTED) */
+#define UFC_VARLEN_AUTO 0        /*   the default: UFC_VARLEN_SORTED8 */
 #define UFC_VARLEN_GENERIC 1     /*   the generic kernel */
-#define UFC_VARLEN_SORTED 2      /*   round-1 kernel on frames sorted by block count within runs of 64 */
-#define UFC_VARLEN_BLOCKED8 3    /*   round-1 kernel, static blocked schedule at 8 waves */
-#define UFC_VARLEN_CLAIM16 4     /*   round-1 kernel, claimed sets at 16 waves (round-1 default) */
-#define UFC_VARLEN_BLOCKSTREAM 5 /*   sorted block-stream kernel (one 1-KB block step at a time) */
+#define UFC_VARLEN_SORTED 2      /*   (tuning) round-1 kernel on frames sorted by block count within runs of 64 */
+#define UFC_VARLEN_BLOCKED8 3    /*   (tuning) round-1 kernel, static blocked schedule at 8 waves */
+#define UFC_VARLEN_CLAIM16 4     /*   (tuning) round-1 kernel, claimed sets at 16 waves (round-1 default) */
+#define UFC_VARLEN_BLOCKSTREAM 5 /*   (tuning) sorted block-stream kernel (one 1-KB block step at a time) */
 #define UFC_VARLEN_SORTED8 6     /*   runs of 64 sorted in the kernel, 8-frame sets of 8 lanes per frame */
 #define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
 #define UFC_OPT_SEAL_KERNEL 3    /* fixed-stride seals: */

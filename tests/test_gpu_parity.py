@@ -567,15 +567,24 @@ def test_fixed_multi_launch(engine, frame_len, extra):
         assert np.array_equal(got, ref_crc)
 
 
-@pytest.mark.parametrize("mode", ["sorted", "blocked8", "generic", "claim16", "blockstream", "sorted8"])
-def test_varlen_alternate_modes(engine, mode):
-    """The varlen kernel's A/B modes (ufc_ctx_set_option): run-sorted records (the default, set
-    explicitly), the static blocked schedule at 8 waves, the generic kernel, the claimed unsorted
-    sets, the block-stream kernel -- mixed lengths, edge lengths, seal, gapped pairs."""
+def test_tuning_only_modes_rejected(engine):
+    """Kernels measured slower than the defaults exist only in -DUFC_TUNING builds: the product
+    library refuses to select them (include/uflow_frame_crc.h, "(tuning)")."""
     from uflow_amd import _native as N
-    value = {"sorted": N.UFC_VARLEN_SORTED, "blocked8": N.UFC_VARLEN_BLOCKED8, "generic": N.UFC_VARLEN_GENERIC,
-             "claim16": N.UFC_VARLEN_CLAIM16, "blockstream": N.UFC_VARLEN_BLOCKSTREAM,
-             "sorted8": N.UFC_VARLEN_SORTED8}[mode]
+    for opt, val in ((N.UFC_OPT_FIXED_KERNEL, N.UFC_FIXED_CLAIM16), (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_SORTED),
+                     (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_BLOCKED8), (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_CLAIM16),
+                     (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_BLOCKSTREAM)):
+        assert N.lib().ufc_ctx_set_option(engine._ctx, opt, val) == N.UFC_ERR_INVALID_ARG
+        assert engine.get_option(opt) == 0
+
+
+@pytest.mark.parametrize("mode", ["generic", "sorted8"])
+def test_varlen_alternate_modes(engine, mode):
+    """The varlen kernel's product modes (ufc_ctx_set_option): the generic kernel and the 8-lane
+    sorted-runs kernel (the default, set explicitly) -- mixed lengths, edge lengths, seal, gapped
+    pairs (pairs run the 8-lane kernel under either)."""
+    from uflow_amd import _native as N
+    value = {"generic": N.UFC_VARLEN_GENERIC, "sorted8": N.UFC_VARLEN_SORTED8}[mode]
     engine.set_option(N.UFC_OPT_VARLEN_KERNEL, value)
     try:
         assert engine.get_option(N.UFC_OPT_VARLEN_KERNEL) == value
@@ -585,16 +594,15 @@ def test_varlen_alternate_modes(engine, mode):
         rng.shuffle(lens)
         _varlen_case(engine, rng, lens, seal=False)
         test_seal_varlen(engine)
-        if mode != "generic":  # (pairs: lean kernel only)
-            test_pairs_gapped_layout(engine)
+        test_pairs_gapped_layout(engine)
     finally:
         engine.set_option(N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_AUTO)
 
 
-@pytest.mark.parametrize("mode", ["generic", "claim16"])
+@pytest.mark.parametrize("mode", ["generic"])
 def test_fixed_alternate_modes(engine, mode):
     from uflow_amd import _native as N
-    value = {"generic": N.UFC_FIXED_GENERIC, "claim16": N.UFC_FIXED_CLAIM16}[mode]
+    value = {"generic": N.UFC_FIXED_GENERIC}[mode]
     engine.set_option(N.UFC_OPT_FIXED_KERNEL, value)
     try:
         rng = np.random.default_rng(92)

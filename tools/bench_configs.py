@@ -12,7 +12,9 @@ parse), one JSON line each.  Not the driver's bench (bench.py is); run on the GP
   host     config 5's GPU leg: 1M x 1472-B frames (uflow's MAX_FRAME_SIZE) that start and end in
            host memory -> ufc_validate_host_varlen (H2D + CRC + D2H) from pinned and from pageable
            buffers; GiB/s of frame bytes including the copies.
-Kernel times are HIP-event medians over --reps launches on the current stream.
+Kernel times: HIP events around groups of 10 back-to-back launches on the current stream (median
+over the groups of --reps launches); ceiling_GBs = ufc_hbm_read_probe (a plain read-only stream) over
+the same buffer, timed the same way.
 """
 import argparse
 import json
@@ -31,18 +33,33 @@ from uflow_amd import synth  # noqa: E402
 from uflow_amd.batch import FrameCrcEngine  # noqa: E402
 
 PEAK = 8e12
+CHECK = True  # --no-check: skip the oracle comparisons and CPU baselines
 
 
-def timed(fn, reps):
+def timed(fn, reps, group=10):
+    """HIP events around groups of `group` back-to-back launches on the current stream (as bench.py:
+    an event pair around every launch adds ~6 us); returns (median, mean) ms per launch over the
+    ceil(reps / group) groups."""
     s = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    ng = max(1, -(-reps // group))
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(ng)]
     for e0, e1 in evs:
         e0.record(s)
-        fn()
+        for _ in range(group):
+            fn()
         e1.record(s)
     torch.cuda.synchronize()
-    t = [a.elapsed_time(b) for a, b in evs]
+    t = [a.elapsed_time(b) / group for a, b in evs]
     return float(np.median(t)), float(np.mean(t))
+
+
+def ceiling(eng, buf, reps):
+    """Read-only streaming ceiling over the same bytes (ufc_hbm_read_probe): GB/s."""
+    sink = torch.zeros(1, dtype=torch.int32, device=buf.device)
+    nbytes = eng.hbm_read_probe(buf, sink)
+    settle(lambda: eng.hbm_read_probe(buf, sink), 20)
+    med, _ = timed(lambda: eng.hbm_read_probe(buf, sink), reps)
+    return round(nbytes / med / 1e-3 / 1e9, 1)
 
 
 def settle(fn, ms=50):
@@ -59,10 +76,15 @@ def threads():
         return os.cpu_count() or 1
 
 
-def rates(name, nbytes, algo, med, mean, **kw):
-    return {"config": name, "kernel_ms": round(med, 4), "kernel_mean_ms": round(mean, 4),
-            "GiB_s": round(nbytes / med / 1e-3 / 2**30, 1), "algo_GB_s": round(algo / med / 1e-3 / 1e9, 1),
-            "hbm_frac": round(algo / med / 1e-3 / PEAK, 4), "algorithmic_bytes": algo, **kw}
+def rates(name, nbytes, algo, med, mean, ceil_gbs=None, **kw):
+    r = {"config": name, "kernel_ms": round(med, 4), "kernel_mean_ms": round(mean, 4),
+         "GiB_s": round(nbytes / med / 1e-3 / 2**30, 1), "algo_GB_s": round(algo / med / 1e-3 / 1e9, 1),
+         "hbm_frac": round(algo / med / 1e-3 / PEAK, 4), "algorithmic_bytes": algo}
+    if ceil_gbs:
+        r["ceiling_GBs"] = ceil_gbs
+        r["frac_of_ceiling"] = round(algo / med / 1e-3 / 1e9 / ceil_gbs, 4)
+    r.update(kw)
+    return r
 
 
 def varlen(eng, dev, reps, n=10_000_000):
@@ -76,18 +98,17 @@ def varlen(eng, dev, reps, n=10_000_000):
     fn()
     torch.cuda.synchronize()
     total = int(offsets[-1])
+    settle(fn)
+    med, mean = timed(fn, reps)
+    ceil_gbs = ceiling(eng, data, reps)
+    algo = total + 8 * (n + 1) + 4 * n + n
+    if not CHECK:
+        return rates("3: varlen 10M x U[64,1500] device-resident (unchecked counter pass)", total, algo, med, mean,
+                     ceil_gbs, frames=n)
     h_data, h_off = data.cpu().numpy(), offsets.cpu().numpy().astype(np.uint64)
     ref_crc, ref_valid = oracle.validate_varlen_mt(h_data, h_off, min(64, threads()))
     exact = bool(np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc) and
                  np.array_equal(valid.cpu().numpy(), ref_valid))
-    settle(fn)
-    med, mean = timed(fn, reps)
-    # A/B: the round-1 kernel (claimed 16-wave sets of 4 consecutive frames) on the same batch
-    from uflow_amd import _native as N
-    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_CLAIM16)
-    settle(fn)
-    med_r1, _ = timed(fn, reps)
-    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_AUTO)
     # CPU baseline: the oracle's bytewise loop (crc.rs:94-100) on the first frames, 1 thread and all
     k1, kn = 50_000, min(n, 50_000 * threads())
 
@@ -98,10 +119,8 @@ def varlen(eng, dev, reps, n=10_000_000):
         return (int(o[-1]) - int(o[0])) / (time.perf_counter() - t0) / 2**30
 
     cpu1, cpun = cpu(k1, 1), cpu(kn, threads())
-    algo = total + 8 * (n + 1) + 4 * n + n
-    return rates("3: varlen 10M x U[64,1500] device-resident", total, algo, med, mean, frames=n, bytes=total,
+    return rates("3: varlen 10M x U[64,1500] device-resident", total, algo, med, mean, ceil_gbs, frames=n, bytes=total,
                  bit_exact_all_frames=exact, valid_count_ok=int(ref_valid.sum()) == n - flipped.numel(),
-                 round1_kernel_ms=round(med_r1, 4),
                  cpu_baseline={"unit": "GiB/s", "single_thread": round(cpu1, 4), "all_threads": round(cpun, 3),
                                "threads": threads(), "nproc": os.cpu_count(),
                                "sample": f"first {k1} frames on 1 thread, first {kn} frames on {threads()} threads"})
@@ -122,7 +141,7 @@ def shard(eng, dev, reps, world=8, rank=3, total=100_000_000, L=1500):
     settle(fn)
     med, mean = timed(fn, reps)
     out = rates(f"4 (one GPU's shard): frames [{lo}, {hi}) of 100M x 1500 B, device-resident", n * L, n * L + 5 * n,
-                med, mean, frames=n, valid_ok=ok)
+                med, mean, ceiling(eng, frames, reps), frames=n, valid_ok=ok)
     del frames
     torch.cuda.empty_cache()
     return out
@@ -149,7 +168,8 @@ def seal(eng, dev, reps, n=1_000_000, L=1500):
         eng.set_option(N.UFC_OPT_SEAL_KERNEL, N.UFC_SEAL_TWO_PASS)
     return rates("2 (encode side): seal 1M x 1500-B frames in place, device-resident (two passes: CRC words, "
                  "then non-temporal trailer stores)", n * L, n * L + 4 * n,
-                 med, mean, frames=n, valid_after_seal=ok, inline_seal_ms=round(med_inline, 4))
+                 med, mean, ceiling(eng, frames, reps), frames=n, valid_after_seal=ok,
+                 inline_seal_ms=round(med_inline, 4))
 
 
 def seal_varlen(eng, dev, reps, n=10_000_000):
@@ -166,7 +186,8 @@ def seal_varlen(eng, dev, reps, n=10_000_000):
     med, mean = timed(fn, reps)
     total = int(offsets[-1])
     return rates("3 (encode side): seal 10M x U[64,1500] frames in place, CSR, device-resident",
-                 total, total + 8 * (n + 1) + 4 * n, med, mean, frames=n, valid_after_seal=ok)
+                 total, total + 8 * (n + 1) + 4 * n, med, mean, ceiling(eng, data, reps), frames=n,
+                 valid_after_seal=ok)
 
 
 def parse(eng, dev, reps, n=1_000_000):
@@ -231,7 +252,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="varlen,shard,seal,seal_varlen,parse,host")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-check", action="store_true",
+                    help="skip the oracle checks and CPU baselines (counter passes of tools/profile_workloads.sh)")
     a = ap.parse_args()
+    global CHECK
+    CHECK = not a.no_check
     dev = torch.device("cuda", 0)
     eng = FrameCrcEngine(0)
     for what in a.only.split(","):

@@ -11,8 +11,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libuflowcrc.so")
-SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_crc_varlen2.hip", "frame_crc_varlen8.hip", "frame_parse.hip", "hbm_probe.hip", "ufc_api.cpp", "ufc_shard.cpp", "crc_math.cpp",
-           "frame_codec.cpp"]
+SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_crc_varlen8.hip", "frame_parse.hip", "hbm_probe.hip",
+           "ufc_api.cpp", "ufc_shard.cpp", "crc_math.cpp", "frame_codec.cpp"]
+# Kernels measured slower than the product's, kept for A/B in tuning builds only.
+TUNING_SOURCES = ["frame_crc_varlen2.hip"]
 HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp", "frame_codec_core.hpp", "frame_parse.hpp",
            "ufc_internal.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -25,14 +27,38 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _digest(paths, extra=()):
+    """sha256 over the named files' contents (and extra strings): the build's identity."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.relpath(p, REPO_DIR).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    for x in extra:
+        h.update(str(x).encode() + b"\0")
+    return h.hexdigest()
+
+
+def _stamp_ok(target, digest):
+    try:
+        with open(target + ".sha256") as f:
+            return os.path.exists(target) and f.read().strip() == digest
+    except OSError:
+        return False
+
+
 def build_native(force=False, verbose=False, tuning=False, out=None, defines=()):
     """tuning=True adds the ablation kernels (-DUFC_TUNING); `defines` adds -D flags (tuning
-    experiments).  Both are meant with `out` pointing away from the product library."""
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    experiments).  Both are meant with `out` pointing away from the product library.
+
+    Rebuilds when the sha256 of the sources, headers, flags and this file differs from the one
+    recorded beside the library (<lib>.sha256), not by file times: a library copied to another
+    machine (the GPU box) with its stamp is rebuilt there only if it does not match the source."""
+    sources = SOURCES + (TUNING_SOURCES if tuning else [])
+    deps = [os.path.join(CSRC, s) for s in sources + HEADERS]
     deps += [os.path.join(REPO_DIR, "include", h) for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
     target = out or LIB_PATH
-    if not force and not _stale(target, deps):
-        return target
     # No atomic optimizer: the lean kernel's single-lane claim atomics must stay plain
     # global_atomic_add (the optimizer reads the result back at once, forcing a vmcnt(0) wait).
     flags = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall",
@@ -40,16 +66,17 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
     if tuning:
         flags.append("-DUFC_TUNING")
     flags += ["-D" + d for d in defines]
-    # One object per source, compiled in parallel, then one link.
+    digest = _digest(deps + [os.path.abspath(__file__)], flags[1:])
+    if not force and _stamp_ok(target, digest):
+        return target
+    # One object per source, compiled in parallel, then one link (every object: the stamp differs).
     objdir = os.path.join(REPO_DIR, "build", "obj_" + os.path.basename(target).replace(".", "_"))
     os.makedirs(objdir, exist_ok=True)
     jobs, objs = [], []
-    hdrs = deps[len(SOURCES):]
-    for src in SOURCES:
+    for src in sources:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
-        if force or _stale(obj, [os.path.join(CSRC, src)] + hdrs + [__file__]):
-            jobs.append(flags + ["-c", os.path.join(CSRC, src), "-o", obj])
+        jobs.append(flags + ["-c", os.path.join(CSRC, src), "-o", obj])
     from concurrent.futures import ThreadPoolExecutor
 
     def run(cmd):
@@ -66,6 +93,8 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
         print(" ".join(link), file=sys.stderr)
     subprocess.run(link, check=True)
     os.replace(target + ".tmp", target)
+    with open(target + ".sha256", "w") as f:
+        f.write(digest + "\n")
     return target
 
 
@@ -75,25 +104,29 @@ LOOPBACK_BIN = os.path.join(REPO_DIR, "tools", "loopback", "ufc_loopback")
 
 def build_tools(force=False, verbose=False):
     """The loopback harness (BASELINE.json configs 1 and 5), linked against the in-tree library."""
-    deps = [LOOPBACK_SRC, LIB_PATH] + [os.path.join(REPO_DIR, "include", h)
-                                        for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
-    if not force and not _stale(LOOPBACK_BIN, deps):
-        return LOOPBACK_BIN
+    deps = [LOOPBACK_SRC] + [os.path.join(REPO_DIR, "include", h) for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
     cmd = [HIPCC, "-O2", "-std=c++17", "-Wall", "-o", LOOPBACK_BIN + ".tmp", LOOPBACK_SRC,
            "-L" + PKG_DIR, "-luflowcrc", "-Wl,-rpath,$ORIGIN/../../uflow_amd", "-lpthread"]
+    digest = _digest(deps + [os.path.abspath(__file__)], cmd[1:])
+    if not force and _stamp_ok(LOOPBACK_BIN, digest):
+        return LOOPBACK_BIN
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(LOOPBACK_BIN + ".tmp", LOOPBACK_BIN)
+    with open(LOOPBACK_BIN + ".sha256", "w") as f:
+        f.write(digest + "\n")
     return LOOPBACK_BIN
 
 
 def build_oracle(force=False):
     odir = os.path.join(REPO_DIR, "oracle")
     target = os.path.join(odir, "liboracle.so")
-    src = os.path.join(odir, "crc_oracle.c")
-    if force or _stale(target, [src]):
-        subprocess.run(["make", "-C", odir, "-s"], check=True)
+    digest = _digest([os.path.join(odir, "crc_oracle.c"), os.path.join(odir, "Makefile")])
+    if force or not _stamp_ok(target, digest):
+        subprocess.run(["make", "-C", odir, "-s", "-B"], check=True)
+        with open(target + ".sha256", "w") as f:
+            f.write(digest + "\n")
     return target
 
 

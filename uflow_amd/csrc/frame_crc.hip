@@ -868,23 +868,27 @@ __global__ __launch_bounds__(WAVES * 64) void fixed_probe_kernel(const KernelPar
 #endif
 
 const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves) {
-  if (abl == 0 && ((depth == 2 && sched == kSchedInterleave && waves == 8) ||
-                   (depth == 3 && sched == kSchedClaim && waves == 16))) {
-    const bool ilv = sched == kSchedInterleave;
+  if (abl == 0 && depth == 2 && sched == kSchedInterleave && waves == 8) {  // the product kernel
     switch (J) {
 #define UFC_PICK_FIXED(JJ)                                                                          \
   case JJ:                                                                                          \
-    if (ilv)                                                                                        \
-      return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 2, 0, kSchedInterleave, 8>        \
-                  : (const void*)frame_crc_fixed_kernel<JJ, false, 2, 0, kSchedInterleave, 8>;      \
-    return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0, kSchedClaim, 16>              \
-                : (const void*)frame_crc_fixed_kernel<JJ, false, 3, 0, kSchedClaim, 16>;
+    return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 2, 0, kSchedInterleave, 8>          \
+                : (const void*)frame_crc_fixed_kernel<JJ, false, 2, 0, kSchedInterleave, 8>;
       UFC_PICK_FIXED(1) UFC_PICK_FIXED(2) UFC_PICK_FIXED(3) UFC_PICK_FIXED(4) UFC_PICK_FIXED(5) UFC_PICK_FIXED(6)
 #undef UFC_PICK_FIXED
       default: return nullptr;
     }
   }
 #ifdef UFC_TUNING
+  // Round-1 default (claimed schedule, 16 waves, depth 3): measured slower, A/B builds only.
+  if (abl == 0 && depth == 3 && sched == kSchedClaim && waves == 16 && J >= 1 && J <= 6) {
+    static const void* const t16[6][2] = {
+#define UFC_C16(JJ) {(const void*)frame_crc_fixed_kernel<JJ, false, 3, 0, kSchedClaim, 16>, \
+                     (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0, kSchedClaim, 16>}
+        UFC_C16(1), UFC_C16(2), UFC_C16(3), UFC_C16(4), UFC_C16(5), UFC_C16(6)};
+#undef UFC_C16
+    return t16[J - 1][seal ? 1 : 0];
+  }
   if (J == 6 && !seal && abl >= 3 && abl <= 4 && (depth == 2 || depth == 3)) {  // loads-only probes
     static const void* const ptab[2][2][2] = {  // [waves 8/16][stage][nbuf 2/3]
         {{(const void*)fixed_probe_kernel<2, 8, false>, (const void*)fixed_probe_kernel<3, 8, false>},

@@ -473,9 +473,11 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen_kernel(const Kern
   template __global__ void frame_crc_varlen_kernel<true, false, 0, SC, WV, SO>(const KernelParams);  \
   template __global__ void frame_crc_varlen_kernel<false, true, 0, SC, WV, SO>(const KernelParams);  \
   template __global__ void frame_crc_varlen_kernel<true, true, 0, SC, WV, SO>(const KernelParams);
+#ifdef UFC_TUNING  // round-1 kernels, measured slower than frame_crc_varlen8.hip: A/B builds only
 UFC_VL_INST(kSchedClaim, 16, true)
 UFC_VL_INST(kSchedClaim, 16, false)
 UFC_VL_INST(kSchedBlocked, 8, false)
+#endif
 
 const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves, bool sorted) {
 #ifdef UFC_TUNING
@@ -503,7 +505,6 @@ const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int 
     if (sched == kSchedClaim && waves == 8) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedClaim, 8, false>;
     if (sched == kSchedBlocked && waves == 16) return (const void*)frame_crc_varlen_kernel<false, false, 0, kSchedBlocked, 16, false>;
   }
-#endif
   if (abl != 0) return nullptr;
 #define UFC_VL_PICK(SC, WV, SO)                                                          \
   if (sched == SC && waves == WV && sorted == SO) {                                      \
@@ -517,6 +518,7 @@ const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int 
   UFC_VL_PICK(kSchedClaim, 16, false)
   UFC_VL_PICK(kSchedBlocked, 8, false)
 #undef UFC_VL_PICK
+#endif  // UFC_TUNING
   return nullptr;
 }
 

@@ -226,6 +226,7 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
   return UFC_OK;
 }
 
+#ifdef UFC_TUNING
 int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream, bool pairs = false) {
   // Claimed sets, 16 waves: measured fastest for mixed lengths (compute-heavy per set; DESIGN.md
   // section 5.2).  UFC_VARLEN_BLOCKED8: the static blocked schedule at 8 waves (A/B).
@@ -286,10 +287,12 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
   }
   return UFC_OK;
 }
+#endif  // UFC_TUNING
 
 // The sorted block-stream kernel (frame_crc_varlen2.hip, UFC_VARLEN_BLOCKSTREAM), CSR batches and pairs.
 // Pairs need the buffer below 2^31 - 1024 bytes (32-bit relative offsets); seal + pairs is not an
 // entry point.  Returns UFC_ERR_INVALID_ARG when the kernel does not apply (the caller falls back).
+#ifdef UFC_TUNING
 int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
   const void* fn = ufc_dev::varlen2_kernel_symbol(seal, pairs);
   if (!fn || (pairs && kp.frame_len >= ((uint64_t)1 << 31) - 1024)) return UFC_ERR_INVALID_ARG;
@@ -317,6 +320,7 @@ int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   }
   return UFC_OK;
 }
+#endif  // UFC_TUNING
 
 // The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): one launch per chunk of
 // < 2^29 frames, each run of 64 frames sorted by block count inside the kernel (tuning builds: the
@@ -410,13 +414,19 @@ int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams
     const int rc = launch_varlen8(ctx, seal, pairs, kp, stream);
     if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the 4-lane kernel below)
   }
+#ifdef UFC_TUNING
   if (opt == UFC_VARLEN_BLOCKSTREAM) {
     const int rc = launch_varlen2(ctx, seal, pairs, kp, stream);
     if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the round-1 kernel below)
   }
+#endif
   if (opt == UFC_VARLEN_GENERIC && !pairs)
     return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen | (seal ? ufc_dev::kModeSeal : 0), kp, stream);
+#ifdef UFC_TUNING
   return launch_lean_varlen(ctx, seal, kp, stream, pairs);
+#else
+  return launch_varlen8(ctx, seal, pairs, kp, stream);  // (pairs under UFC_VARLEN_GENERIC)
+#endif
 }
 
 using ufc_internal::kMaxFrameLen;
@@ -479,9 +489,16 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
   switch (option) {
     case UFC_OPT_FIXED_KERNEL:
       if (value < UFC_FIXED_AUTO || value > UFC_FIXED_CLAIM16) return UFC_ERR_INVALID_ARG;
+#ifndef UFC_TUNING
+      if (value == UFC_FIXED_CLAIM16) return UFC_ERR_INVALID_ARG;  // (A/B kernel of tuning builds)
+#endif
       break;
     case UFC_OPT_VARLEN_KERNEL:
       if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_SORTED8) return UFC_ERR_INVALID_ARG;
+#ifndef UFC_TUNING
+      if (value != UFC_VARLEN_AUTO && value != UFC_VARLEN_GENERIC && value != UFC_VARLEN_SORTED8)
+        return UFC_ERR_INVALID_ARG;  // (round-1 and block-stream kernels: A/B in tuning builds)
+#endif
       break;
     case UFC_OPT_GENERIC_JC:
       if (value != 0 && !ufc_dev::config_available(value)) return UFC_ERR_INVALID_ARG;
