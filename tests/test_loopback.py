@@ -26,10 +26,14 @@ def test_echo_plumbing():
     assert j["echoes_ok"] == j["messages"] == 10
 
 
-def _check_stream(j, n, every):
+def _check_stream(j, n, every, max_loss=None):
     assert j["payload_mismatch"] == 0
     assert j["received"] > 0 and j["valid"] + j["invalid"] == j["received"]
     assert j["parsed"] == j["valid"]
+    if "lost" in j:
+        assert j["lost"] == j["sent"] - j["received"]
+    if max_loss is not None:  # paced senders: the gate must keep up (ideal_transfer.rs: all arrives)
+        assert j["loss_frac"] <= max_loss, j
     if j["received"] == n:  # nothing dropped by the socket: exactly the corrupted frames fail
         assert j["invalid"] == n // every
 
@@ -51,10 +55,24 @@ def test_stream_inline_cpu_gate():
     _check_stream(_run(["--gate", "cpu", "--rx-threads", "2", "--frames", str(n), "--corrupt-every", "997"]), n, 997)
 
 
+def test_stream_inline_cpu_gate_paced():
+    """Paced senders (0.1 GB/s offered, a rate this container's CPU gate keeps up with): loss is
+    reported (sent - received) and stays under 0.5 %."""
+    n = 60_000
+    j = _run(["--gate", "cpu", "--rx-threads", "2", "--tx-per-rx", "1", "--frames", str(n), "--corrupt-every", "997",
+              "--rate-gbps", "0.1"])
+    _check_stream(j, n, 997, max_loss=0.005)
+
+
 @pytest.mark.gpu
 def test_stream_inline_gpu_gate():
-    """The same with the asynchronous GPU gate overlapped with the next receive."""
+    """The same with the asynchronous GPU gate overlapped with the next receive: unpaced (loss
+    reported, not bounded) and paced at 0.8 GB/s, where the loss must stay under 0.5 %."""
     n = 200_000
     j = _run(["--gate", "gpu", "--rx-threads", "2", "--frames", str(n), "--corrupt-every", "997"])
     assert j["failed_threads"] == 0
     _check_stream(j, n, 997)
+    j = _run(["--gate", "gpu", "--rx-threads", "2", "--tx-per-rx", "1", "--frames", str(n), "--corrupt-every", "997",
+              "--rate-gbps", "0.8"])
+    assert j["failed_threads"] == 0
+    _check_stream(j, n, 997, max_loss=0.005)

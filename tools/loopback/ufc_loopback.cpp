@@ -122,7 +122,20 @@ struct Args {
   int send_seal = 0;  // 0: frames built once and re-sent; 1: built per flush, sealed on the CPU; 2: ... on the GPU
   int rx_threads = 0;  // > 0: the inline receive loop on that many threads (run_stream_inline)
   int tx_per_rx = 1;   // sender threads per receive thread (inline mode)
+  double rate_gbps = 0;  // inline mode: offered rate of frame bytes, all senders together (0 = unpaced)
 };
+
+// Sender pacing: block until `bytes` may leave at `rate` B/s counted from t0 (spin for short waits).
+void pace(double t0, double bytes, double rate) {
+  if (rate <= 0) return;
+  const double due = t0 + bytes / rate;
+  for (;;) {
+    const double d = due - now_s();
+    if (d <= 0) return;
+    if (d > 200e-6) std::this_thread::sleep_for(std::chrono::duration<double>(d - 100e-6));
+    else std::this_thread::yield();
+  }
+}
 
 // ---------------- config 1: echo plumbing ----------------
 int run_echo(const Args& a) {
@@ -456,12 +469,15 @@ int run_stream(const Args& a) {
   const double secs = now_s() - t_first;
   const double span = std::max(t_last - t_first, 1e-9);
   printf("{\"config\": \"5: ideal_transfer-style loopback at saturation, %s CRC gate in the receive path\", "
-         "\"frame_bytes\": %zu, \"sent\": %llu, \"received\": %llu, \"valid\": %llu, \"invalid\": %llu, "
+         "\"frame_bytes\": %zu, \"sent\": %llu, \"received\": %llu, \"lost\": %llu, \"loss_frac\": %.5f, "
+         "\"valid\": %llu, \"invalid\": %llu, "
          "\"parsed\": %llu, \"payload_mismatch\": %llu, \"receive_seconds\": %.4f, \"frames_per_s\": %.0f, "
          "\"GB_s\": %.3f, \"gate_seconds\": %.4f, \"gate_GB_s\": %.3f, \"batch\": %d, \"total_seconds\": %.4f, "
          "\"send_seal\": \"%s\", \"send_seal_seconds\": %.4f, \"send_seal_GB_s\": %.3f, \"send_seconds\": %.4f}\n",
          a.gpu ? "GPU (ufc_validate_host_slots: H2D + kernel + D2H)" : "CPU (ufc_frame_validate, 1 thread)", kFrame,
-         (unsigned long long)sent.load(), (unsigned long long)received, (unsigned long long)n_valid,
+         (unsigned long long)sent.load(), (unsigned long long)received,
+         (unsigned long long)(sent.load() - std::min<uint64_t>(sent.load(), received)),
+         sent.load() ? 1.0 - (double)received / (double)sent.load() : 0.0, (unsigned long long)n_valid,
          (unsigned long long)n_invalid, (unsigned long long)n_parsed, (unsigned long long)n_payload_bad, span,
          received / span, bytes_in / span / 1e9, t_gate, t_gate > 0 ? bytes_in / t_gate / 1e9 : 0.0, a.batch, secs,
          a.send_seal == 0 ? "none (prebuilt frames)" : a.send_seal == 1 ? "cpu (ufc_frame_seal per frame)"
@@ -483,7 +499,7 @@ int run_stream(const Args& a) {
 // ---------------- config 5, inline receive loops on R threads ----------------
 struct LaneStats {
   uint64_t received = 0, valid = 0, invalid = 0, parsed = 0, payload_bad = 0, bytes = 0;
-  double t_first = 0, t_last = 0, t_gate = 0;
+  double t_first = 0, t_last = 0, t_gate = 0, t_recv = 0, t_handle = 0, t_sync = 0;
 };
 
 int run_stream_inline(const Args& a) {
@@ -505,6 +521,10 @@ int run_stream_inline(const Args& a) {
     getsockopt(rx[r], SOL_SOCKET, SO_RCVBUF, &rcvbuf, &sl);
   }
   const int TX = R * std::max(1, a.tx_per_rx);
+  const double rate_tx = a.rate_gbps > 0 ? a.rate_gbps * 1e9 / TX : 0.0;  // B/s per sender
+  std::atomic<uint64_t> sent_total{0};
+  const double t_send0 = now_s();  // (pacing clock and the sender-clock goodput start)
+  std::vector<double> t_send_end(TX, 0.0);
   for (int t = 0; t < TX; t++) {
     // sender t: frames [F t / TX, F (t+1) / TX) to port + t % R
     threads.emplace_back([&, t] {
@@ -517,6 +537,7 @@ int run_stream_inline(const Args& a) {
       std::vector<uint8_t> scratch((size_t)M * kFrame);
       for (uint64_t s = lo; s < hi;) {
         const int m = (int)std::min<uint64_t>(M, hi - s);
+        pace(t_send0, (double)(s - lo) * kFrame, rate_tx);
         for (int i = 0; i < m; i++) {
           const uint64_t q = s + i;
           uint8_t* f = ring.data() + (size_t)(q % kRing) * kFrame;
@@ -534,8 +555,12 @@ int run_stream_inline(const Args& a) {
           msgs[i].msg_hdr.msg_iovlen = 1;
         }
         const int k = sendmmsg(tx, msgs.data(), m, 0);
-        if (k > 0) s += (uint64_t)k;
+        if (k > 0) {
+          s += (uint64_t)k;
+          sent_total += (uint64_t)k;
+        }
       }
+      t_send_end[t] = now_s();
       close(tx);
       senders_done++;
     });
@@ -623,7 +648,9 @@ int run_stream_inline(const Args& a) {
             msgs[i].msg_hdr.msg_iov = &iov[i];
             msgs[i].msg_hdr.msg_iovlen = 1;
           }
+          const double tr0 = now_s();
           const int k = recvmmsg(rx[r], msgs.data(), (unsigned)want, MSG_WAITFORONE, nullptr);
+          if (k > 0) S.t_recv += now_s() - tr0;
           if (k <= 0) {  // 300 ms without a datagram
             if (senders_done.load() == TX) {
               idle = true;
@@ -643,9 +670,13 @@ int run_stream_inline(const Args& a) {
           if (b.n && ufc_validate_host_slots_async(ctx, b.slots, kFrame, b.lens, b.n, b.crc, b.valid, streams[cur]) != UFC_OK)
             return fail("ufc_validate_host_slots_async");
           if (pending >= 0) {
+            const double ts = now_s();
             if (hipStreamSynchronize(streams[pending]) != hipSuccess) return fail("hipStreamSynchronize");
+            S.t_sync += now_s() - ts;
             S.t_gate += now_s() - t0;  // (queueing + waiting: the gate's cost to this thread)
+            const double th = now_s();
             handle(bufs[pending]);
+            S.t_handle += now_s() - th;
           } else {
             S.t_gate += now_s() - t0;
           }
@@ -655,7 +686,9 @@ int run_stream_inline(const Args& a) {
           const double t0 = now_s();
           for (size_t i = 0; i < b.n; i++) b.valid[i] = (uint8_t)ufc_frame_validate(b.slots + i * kFrame, b.lens[i]);
           S.t_gate += now_s() - t0;
+          const double th = now_s();
           handle(b);
+          S.t_handle += now_s() - th;
         }
       }
       if (pending >= 0) {
@@ -696,19 +729,34 @@ int run_stream_inline(const Args& a) {
       T.t_last = std::max(T.t_last, S.t_last);
     }
     T.t_gate += S.t_gate;
+    T.t_recv += S.t_recv;
+    T.t_handle += S.t_handle;
+    T.t_sync += S.t_sync;
     gate_max = std::max(gate_max, S.t_gate);
   }
   const double span = std::max(T.t_last - T.t_first, 1e-9);
-  printf("{\"config\": \"5: ideal_transfer-style loopback at saturation, inline receive loops (receive + %s gate + "
+  double send_end = t_send0;
+  for (double t : t_send_end) send_end = std::max(send_end, t);
+  const uint64_t sent = sent_total.load();
+  // Goodput on the senders' clock: frame bytes received / (last datagram received - first sent):
+  // comparable between gates whatever each one dropped (ideal_transfer.rs).
+  const double span_tx = std::max((T.received ? T.t_last : send_end) - t_send0, 1e-9);
+  printf("{\"config\": \"5: ideal_transfer-style loopback, inline receive loops (receive + %s gate + "
          "parse + payload check per thread)\", \"rx_threads\": %d, \"frame_bytes\": %zu, \"sent\": %llu, "
-         "\"received\": %llu, \"valid\": %llu, \"invalid\": %llu, \"parsed\": %llu, \"payload_mismatch\": %llu, "
-         "\"receive_seconds\": %.4f, \"frames_per_s\": %.0f, \"GB_s\": %.3f, \"gate_thread_seconds\": %.4f, "
-         "\"gate_share_of_thread_time\": %.3f, \"batch\": %d, \"failed_threads\": %d, \"tx_threads\": %d, "
+         "\"received\": %llu, \"lost\": %llu, \"loss_frac\": %.5f, \"offered_GB_s\": %.3f, "
+         "\"valid\": %llu, \"invalid\": %llu, \"parsed\": %llu, \"payload_mismatch\": %llu, "
+         "\"receive_seconds\": %.4f, \"frames_per_s\": %.0f, \"GB_s\": %.3f, \"goodput_GB_s_sender_clock\": %.3f, "
+         "\"send_seconds\": %.4f, \"gate_thread_seconds\": %.4f, "
+         "\"gate_share_of_thread_time\": %.3f, \"recv_call_seconds\": %.4f, \"sync_wait_seconds\": %.4f, "
+         "\"handle_seconds\": %.4f, \"batch\": %d, \"failed_threads\": %d, \"tx_threads\": %d, "
          "\"so_rcvbuf\": %d}\n",
          a.gpu ? "GPU (ufc_validate_host_slots_async, overlapped with the next receive)" : "CPU (ufc_frame_validate)", R,
-         kFrame, (unsigned long long)a.frames, (unsigned long long)T.received, (unsigned long long)T.valid,
+         kFrame, (unsigned long long)sent, (unsigned long long)T.received,
+         (unsigned long long)(sent - std::min(sent, T.received)), sent ? 1.0 - (double)T.received / (double)sent : 0.0,
+         a.rate_gbps, (unsigned long long)T.valid,
          (unsigned long long)T.invalid, (unsigned long long)T.parsed, (unsigned long long)T.payload_bad, span,
-         T.received / span, T.bytes / span / 1e9, T.t_gate, T.t_gate / (span * R), a.batch, failed.load(), TX, rcvbuf);
+         T.received / span, T.bytes / span / 1e9, T.bytes / span_tx / 1e9, send_end - t_send0, T.t_gate,
+         T.t_gate / (span * R), T.t_recv, T.t_sync, T.t_handle, a.batch, failed.load(), TX, rcvbuf);
   return (T.payload_bad == 0 && T.received > 0 && failed.load() == 0) ? 0 : 1;
 }
 
@@ -728,13 +776,15 @@ int main(int argc, char** argv) {
     else if (s == "--no-verify") a.verify = false;
     else if (s == "--rx-threads") a.rx_threads = atoi(next());
     else if (s == "--tx-per-rx") a.tx_per_rx = atoi(next());
+    else if (s == "--rate-gbps") a.rate_gbps = atof(next());
     else if (s == "--send-seal") {
       const std::string v = next();
       a.send_seal = v == "gpu" ? 2 : v == "cpu" ? 1 : 0;
     }
     else {
       fprintf(stderr, "usage: %s [--echo] [--gate gpu|cpu] [--frames N] [--batch B] [--port P] "
-                      "[--corrupt-every K] [--no-verify] [--send-seal none|cpu|gpu] [--rx-threads R]\n", argv[0]);
+                      "[--corrupt-every K] [--no-verify] [--send-seal none|cpu|gpu] [--rx-threads R] [--tx-per-rx T] "
+                      "[--rate-gbps G]\n", argv[0]);
       return 2;
     }
   }

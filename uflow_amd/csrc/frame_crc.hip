@@ -807,14 +807,12 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
 #endif
 }
 
-// Product configurations: the default (interleaved schedule, 8 waves, depth 2; measured fastest,
-// DESIGN.md section 5.1) and the claimed schedule at 16 waves / depth 3 (the previous default, kept
-// for A/B through UFC_LEAN_CFG=claim16).
+// Product configuration: interleaved schedule, 8 waves, depth 2 (measured fastest, DESIGN.md
+// section 5.1).  The claimed schedule at 16 waves / depth 3 (the round-1 default) is instantiated
+// only in tuning builds (fixed_kernel_symbol, UFC_FIXED_CLAIM16).
 #define UFC_INST_FIXED(J)                                                                                  \
   template __global__ void frame_crc_fixed_kernel<J, false, 2, 0, kSchedInterleave, 8>(const KernelParams); \
-  template __global__ void frame_crc_fixed_kernel<J, true, 2, 0, kSchedInterleave, 8>(const KernelParams);  \
-  template __global__ void frame_crc_fixed_kernel<J, false, 3, 0, kSchedClaim, 16>(const KernelParams);     \
-  template __global__ void frame_crc_fixed_kernel<J, true, 3, 0, kSchedClaim, 16>(const KernelParams);
+  template __global__ void frame_crc_fixed_kernel<J, true, 2, 0, kSchedInterleave, 8>(const KernelParams);
 UFC_INST_FIXED(1) UFC_INST_FIXED(2) UFC_INST_FIXED(3) UFC_INST_FIXED(4) UFC_INST_FIXED(5) UFC_INST_FIXED(6)
 
 #ifdef UFC_TUNING

@@ -376,10 +376,11 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     const uint32_t crc = ~unshift(group_lin8(L, c), geo);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
     const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
-    if (SEAL && L.col >= 4u && !((geo >> 22) & 1u)) {  // BE32 trailer: lane 4 + k writes byte k
-      const uint32_t k = L.col - 4u;
-      st_u8_hidden((uint8_t*)p.wbytes + sb + (voff0 - 16u * L.col + 256u * v8_J(geo) - v8_t(geo) - 4u + k),
-                   crc >> (24 - 8 * k));
+    if (SEAL && L.col == 7u && !((geo >> 22) & 1u)) {  // BE32 trailer: one dword store from lane 7
+      // (4-byte aligned when t = 0; otherwise an unaligned dword store, which gfx950's unaligned access
+      // mode splits in the memory pipeline: one store instruction per frame instead of four byte stores)
+      st_u32_hidden((uint32_t*)((uint8_t*)p.wbytes + sb + (voff0 - 16u * L.col + 256u * v8_J(geo) - v8_t(geo) - 4u)),
+                    __builtin_bswap32(crc));
     }
     record(q & 7u, crc, v8_orig(geo) | (ok << 31) | (((geo >> 22) & 1u) << 30));
     if ((q & 7u) == 7u) store_run(q >> 3);
