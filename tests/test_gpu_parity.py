@@ -578,13 +578,13 @@ def test_tuning_only_modes_rejected(engine):
         assert engine.get_option(opt) == 0
 
 
-@pytest.mark.parametrize("mode", ["generic", "sorted8"])
+@pytest.mark.parametrize("mode", ["generic", "sorted8", "stream"])
 def test_varlen_alternate_modes(engine, mode):
-    """The varlen kernel's product modes (ufc_ctx_set_option): the generic kernel and the 8-lane
-    sorted-runs kernel (the default, set explicitly) -- mixed lengths, edge lengths, seal, gapped
-    pairs (pairs run the 8-lane kernel under either)."""
+    """The varlen kernel's product modes (ufc_ctx_set_option): the generic kernel, the 8-lane
+    sorted-runs kernel and the byte-balanced streaming kernel -- mixed lengths, edge lengths, seal,
+    gapped pairs (pairs always run the 8-lane kernel)."""
     from uflow_amd import _native as N
-    value = {"generic": N.UFC_VARLEN_GENERIC, "sorted8": N.UFC_VARLEN_SORTED8}[mode]
+    value = {"generic": N.UFC_VARLEN_GENERIC, "sorted8": N.UFC_VARLEN_SORTED8, "stream": N.UFC_VARLEN_STREAM}[mode]
     engine.set_option(N.UFC_OPT_VARLEN_KERNEL, value)
     try:
         assert engine.get_option(N.UFC_OPT_VARLEN_KERNEL) == value

@@ -102,9 +102,25 @@ def varlen(eng, dev, reps, n=10_000_000):
     med, mean = timed(fn, reps)
     ceil_gbs = ceiling(eng, data, reps)
     algo = total + 8 * (n + 1) + 4 * n + n
+    # A/B: the other variable-length kernel on the same batch (sorted-runs 8-lane sets vs byte streams)
+    from uflow_amd import _native as N
+    other = N.UFC_VARLEN_SORTED8 if eng.get_option(N.UFC_OPT_VARLEN_KERNEL) in (N.UFC_VARLEN_STREAM,) else N.UFC_VARLEN_STREAM
+    saved = eng.get_option(N.UFC_OPT_VARLEN_KERNEL)
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, other)
+    crc2 = torch.empty(n, dtype=torch.int32, device=dev)
+    valid2 = torch.empty(n, dtype=torch.uint8, device=dev)
+    fn2 = lambda: eng.crc_varlen(data, offsets, crc_out=crc2, valid_out=valid2)  # noqa: E731
+    fn2()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(crc, crc2) and torch.equal(valid, valid2))
+    settle(fn2)
+    med2, _ = timed(fn2, reps)
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, saved)
+    ab = {"other_kernel": "stream" if other == N.UFC_VARLEN_STREAM else "sorted8", "other_kernel_ms": round(med2, 4),
+          "other_equal_results": same}
     if not CHECK:
         return rates("3: varlen 10M x U[64,1500] device-resident (unchecked counter pass)", total, algo, med, mean,
-                     ceil_gbs, frames=n)
+                     ceil_gbs, frames=n, **ab)
     h_data, h_off = data.cpu().numpy(), offsets.cpu().numpy().astype(np.uint64)
     ref_crc, ref_valid = oracle.validate_varlen_mt(h_data, h_off, min(64, threads()))
     exact = bool(np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc) and
@@ -120,7 +136,7 @@ def varlen(eng, dev, reps, n=10_000_000):
 
     cpu1, cpun = cpu(k1, 1), cpu(kn, threads())
     return rates("3: varlen 10M x U[64,1500] device-resident", total, algo, med, mean, ceil_gbs, frames=n, bytes=total,
-                 bit_exact_all_frames=exact, valid_count_ok=int(ref_valid.sum()) == n - flipped.numel(),
+                 bit_exact_all_frames=exact, valid_count_ok=int(ref_valid.sum()) == n - flipped.numel(), **ab,
                  cpu_baseline={"unit": "GiB/s", "single_thread": round(cpu1, 4), "all_threads": round(cpun, 3),
                                "threads": threads(), "nproc": os.cpu_count(),
                                "sample": f"first {k1} frames on 1 thread, first {kn} frames on {threads()} threads"})
@@ -250,6 +266,8 @@ def host(eng, reps=5, n=1_000_000, L=1472):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--varlen-kernel", default="auto", choices=["auto", "sorted8", "stream"],
+                    help="variable-length kernel of the timed runs (the other one is timed beside it)")
     ap.add_argument("--only", default="varlen,shard,seal,seal_varlen,parse,host")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-check", action="store_true",
@@ -259,6 +277,9 @@ def main():
     CHECK = not a.no_check
     dev = torch.device("cuda", 0)
     eng = FrameCrcEngine(0)
+    from uflow_amd import _native as N
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, {"auto": N.UFC_VARLEN_AUTO, "sorted8": N.UFC_VARLEN_SORTED8,
+                                             "stream": N.UFC_VARLEN_STREAM}[a.varlen_kernel])
     for what in a.only.split(","):
         if what == "host":
             for r in host(eng):

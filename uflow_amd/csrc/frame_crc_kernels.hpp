@@ -81,6 +81,11 @@ const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // p.offsets = sort_runs records (tuning builds only, A/B).  Pairs need the buffer below
 // 2^31 - 2^20 bytes (32-bit offsets from the buffer).
 const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort);
+// Byte-balanced streaming kernel (frame_crc_varlen8.hip): CSR batches, 12 waves per workgroup, one
+// workgroup per CU; tables as the 8-lane kernel (A^128 chains, the 32-slot nibble image).  A launch
+// covers fewer than 2^31 frames.
+constexpr int kStreamWaves = 12;
+const void* stream8_kernel_symbol(bool seal);
 // Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride
 // + lens[i] (ufc_validate_host_slots_async).
 int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream);

@@ -387,6 +387,31 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   return UFC_OK;
 }
 
+// The byte-balanced streaming kernel (frame_crc_varlen8.hip, frame_crc_stream8_kernel): CSR batches,
+// one launch per chunk of < 2^29 frames (offsets stay absolute; a chunk shifts the offsets and outputs).
+int launch_stream8(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
+  const void* fn = ufc_dev::stream8_kernel_symbol(seal);
+  if (!fn) return UFC_ERR_INVALID_ARG;
+  kp.chain_tab = ctx->d_chain128;
+  kp.nib_img = ctx->d_nib32;
+  kp.G = ctx->G;
+  const uint64_t chunk = (uint64_t)1 << 29;
+  const uint64_t total = kp.nframes;
+  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
+    ufc_dev::KernelParams c = kp;
+    c.nframes = std::min(chunk, total - f0);
+    c.offsets = kp.offsets + f0;
+    c.offsets_csr = c.offsets;
+    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
+    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
+    void* args[] = {&c};
+    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)ctx->ncu), dim3((unsigned)(ufc_dev::kStreamWaves * 64)),
+                                         args, 0, stream);
+    if (e != hipSuccess) return hip_fail(ctx, e);
+  }
+  return UFC_OK;
+}
+
 // Variable-length batches: the sorted-runs kernel by default; the claimed 16-wave and blocked 8-wave
 // schedules, the block-stream kernel and the generic kernel by option.
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream);
@@ -410,7 +435,8 @@ Config varlen_config(const ufc_ctx* ctx) {
 
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
   const int opt = ctx->opt[UFC_OPT_VARLEN_KERNEL];
-  if (opt == UFC_VARLEN_SORTED8 || opt == UFC_VARLEN_AUTO) {
+  if (opt == UFC_VARLEN_STREAM && !pairs) return launch_stream8(ctx, seal, kp, stream);
+  if (opt == UFC_VARLEN_SORTED8 || opt == UFC_VARLEN_AUTO || opt == UFC_VARLEN_STREAM) {
     const int rc = launch_varlen8(ctx, seal, pairs, kp, stream);
     if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the 4-lane kernel below)
   }
@@ -494,9 +520,10 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
 #endif
       break;
     case UFC_OPT_VARLEN_KERNEL:
-      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_SORTED8) return UFC_ERR_INVALID_ARG;
+      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_STREAM) return UFC_ERR_INVALID_ARG;
 #ifndef UFC_TUNING
-      if (value != UFC_VARLEN_AUTO && value != UFC_VARLEN_GENERIC && value != UFC_VARLEN_SORTED8)
+      if (value != UFC_VARLEN_AUTO && value != UFC_VARLEN_GENERIC && value != UFC_VARLEN_SORTED8 &&
+          value != UFC_VARLEN_STREAM)
         return UFC_ERR_INVALID_ARG;  // (round-1 and block-stream kernels: A/B in tuning builds)
 #endif
       break;
