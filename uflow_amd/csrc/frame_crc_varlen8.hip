@@ -703,13 +703,14 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_stream8_kernel(const Ker
         raw_load(wfb + 16, RS, RE);
       }
     }
-    if (__builtin_amdgcn_ballot_w64(adv) != 0) {
+    if (__builtin_amdgcn_ballot_w64(adv) != 0) {  // (take_geo's bpermutes need every lane active)
       const uint32_t pg = lg, pw = lw, pk = lk;
+      const bool pd = ldone;
       take_geo();
       lg = adv ? lg : pg;
       lw = adv ? lw : pw;
       lk = adv ? lk : pk;
-      ldone = adv ? (lg & kSgEnd) != 0 : ldone;
+      ldone = adv ? ldone : pd;
     }
   };
 
