@@ -663,3 +663,21 @@ def test_fixed_random_shapes(engine):
         engine.seal_fixed(d[shift:], frame_len, stride=stride, n=n)
         torch.cuda.synchronize()
         assert np.array_equal(d.cpu().numpy()[shift:], sealed), ctx
+
+
+def test_release_stream_scratch(engine):
+    """ufc_ctx_release_stream frees a stream's scratch (here the parse's); the next parse on that
+    stream allocates it again and gives the same result."""
+    import torch
+    frames, data, offsets = _codec_batch(12, 500)
+    d = torch.from_numpy(data).to(DEV)
+    o = torch.from_numpy(offsets).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        a = [t.cpu() for t in engine.parse_varlen(d, o, valid, stream=s)]
+    engine.release_stream(s)
+    with torch.cuda.stream(s):
+        b = [t.cpu() for t in engine.parse_varlen(d, o, valid, stream=s)]
+    engine.release_stream(s)
+    assert all(torch.equal(x, y) for x, y in zip(a, b))

@@ -40,6 +40,7 @@ _SIGNATURES = {
     "ufc_device_count": (ctypes.c_int, []),
     "ufc_ctx_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int]),
     "ufc_ctx_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_ctx_release_stream": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "ufc_error_string": (ctypes.c_char_p, [ctypes.c_int]),
     "ufc_ctx_last_hip_error": (ctypes.c_int, [ctypes.c_void_p]),
     "ufc_ctx_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]),

@@ -40,6 +40,11 @@ class FrameCrcEngine:
         except Exception:
             pass
 
+    def release_stream(self, stream):
+        """ufc_ctx_release_stream: free this context's scratch kept for `stream` (a torch.cuda.Stream)
+        after the work queued on it; call before the stream goes away."""
+        check(lib().ufc_ctx_release_stream(self._ctx, ctypes.c_void_p(stream.cuda_stream)), "ufc_ctx_release_stream")
+
     def set_option(self, option, value):
         """ufc_ctx_set_option (A/B kernel selection; results never depend on it)."""
         check(lib().ufc_ctx_set_option(self._ctx, int(option), int(value)), "ufc_ctx_set_option")

@@ -600,6 +600,32 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
   return UFC_OK;
 }
 
+int ufc_ctx_release_stream(ufc_ctx* ctx, void* stream) {
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  DeviceGuard g(ctx->device);
+  std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+  bool synced = false;
+  int rc = UFC_OK;
+  for (size_t i = 0; i < ctx->scratch.size();) {
+    ufc_ctx::Scratch& sc = ctx->scratch[i];
+    if (sc.stream != (hipStream_t)stream) {
+      i++;
+      continue;
+    }
+    if (!synced) {  // the work queued on the stream may still use its scratch
+      const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+      if (e != hipSuccess) {
+        rc = hip_fail(ctx, e);
+        break;
+      }
+      synced = true;
+    }
+    if (sc.p) (void)hipFree(sc.p);
+    ctx->scratch.erase(ctx->scratch.begin() + (long)i);
+  }
+  return rc;
+}
+
 int ufc_ctx_destroy(ufc_ctx* ctx) {
   if (!ctx) return UFC_OK;
   {
