@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstddef>
 
 #include "frame_codec_core.hpp"
@@ -91,12 +92,16 @@ __device__ __forceinline__ uint32_t frame_len32(const uint64_t* offsets, uint64_
 __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t* bytes, const uint64_t* offsets,
                                                                    uint64_t n, const uint8_t* valid,
                                                                    ufc_frame_info* infos, uint32_t* counts,
-                                                                   uint8_t* modes, uint16_t* pos_seg) {
+                                                                   uint8_t* modes, uint16_t* pos_seg,
+                                                                   uint32_t* seg_cursor, uint32_t* seg_base,
+                                                                   uint64_t seg_cap) {
   __shared__ uint16_t slots[kSegWords];
   __shared__ typename BlockScan::TempStorage scan_tmp;
+  __shared__ uint32_t base_lds;
   const uint32_t t = threadIdx.x;
   const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + t;
   uint32_t npos = 0;
+  uint8_t mode = kItemsNone;
   if (i < n) {
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
@@ -104,7 +109,6 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
     const bool ok = ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[i] != 0, info, PosSink{slots + t},
                                              kPosSlots);
     const uint32_t cnt = ok ? info.item_count : 0u;
-    uint8_t mode = kItemsNone;
     if (cnt) {
       if (info.kind == UFC_FRAME_ACK) {
         mode = kItemsAck;
@@ -118,19 +122,30 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
     info.item_first = 0;  // written by the emit step
     infos[i] = info;
     counts[i] = cnt;
-    modes[i] = mode;
   }
-  uint32_t lo;
-  BlockScan(scan_tmp).ExclusiveSum(npos, lo);
-  // (each thread reads back only the slots it wrote)
-  uint16_t* seg = pos_seg + (uint64_t)blockIdx.x * kSegWords;
-  for (uint32_t k = 0; k < npos; k++) seg[lo + k] = slots[k * kParseThreads + t];
+  uint32_t lo, total;
+  BlockScan(scan_tmp).ExclusiveSum(npos, lo, total);
+  // the workgroup's segment of header slots, from the launch's bump counter (no room: the emit
+  // step re-walks this workgroup's frames instead)
+  if (t == 0) {
+    uint32_t b = total ? atomicAdd(seg_cursor, total) : 0u;
+    if (total && (uint64_t)b + total > seg_cap) b = 0xFFFFFFFFu;
+    base_lds = b;
+    seg_base[blockIdx.x] = b;
+  }
+  __syncthreads();
+  const uint32_t base = base_lds;
+  if (i < n) modes[i] = (mode == kItemsPos && base == 0xFFFFFFFFu) ? (uint8_t)kItemsWalk : mode;
+  if (base != 0xFFFFFFFFu) {  // (each thread reads back only the slots it wrote)
+    uint16_t* seg = pos_seg + base;
+    for (uint32_t k = 0; k < npos; k++) seg[lo + k] = slots[k * kParseThreads + t];
+  }
 }
 
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
-    const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg, ufc_item* items,
-    uint64_t cap, uint64_t* items_used) {
+    const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
+    const uint32_t* seg_base, ufc_item* items, uint64_t cap, uint64_t* items_used) {
   __shared__ uint32_t lfirst[kParseThreads], lseg[kParseThreads];
   __shared__ uint64_t lstart[kParseThreads];
   __shared__ uint8_t lmode[kParseThreads];
@@ -172,7 +187,8 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
       __builtin_amdgcn_make_buffer_rsrc((void*)(base_addr - delta), 0, buf_ok ? (int)(uint32_t)range : 0, 0x00020000);
 
   const uint32_t g0 = lfirst[0], g1 = lend;
-  const uint16_t* seg = pos_seg + (uint64_t)blockIdx.x * kSegWords;
+  const uint32_t sb = seg_base[blockIdx.x];  // (0xFFFFFFFF: no segment, and no kItemsPos frame either)
+  const uint16_t* seg = pos_seg + (sb == 0xFFFFFFFFu ? 0u : sb);
   if (items) {
     for (uint32_t g = g0 + t; g < g1 && (uint64_t)g < cap; g += kParseThreads) {
       uint32_t lo_f = 0, hi_f = nb - 1;  // owner: the last frame whose first item is <= g
@@ -230,34 +246,58 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
 
 }  // namespace
 
-size_t parse_scratch_bytes(uint64_t n) {
+namespace {
+struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned parts)
+  uint64_t counts, firsts, modes, cursor, bases, slots, temp, end, seg_cap;
+  ParseLayout(uint64_t n, uint64_t items_cap, size_t temp_bytes) {
+    auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
+    const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
+    seg_cap = std::min<uint64_t>(n * kPosSlots, std::max<uint64_t>(items_cap, 1));  // u16 header slots
+    counts = 0;
+    firsts = counts + up(n * 4);
+    modes = firsts + up(n * 4);
+    cursor = modes + up(n);
+    bases = cursor + 256;
+    slots = bases + up(blocks * 4);
+    temp = slots + up(seg_cap * 2);
+    end = temp + up(temp_bytes);
+  }
+};
+size_t scan_temp_bytes(uint64_t n) {
   size_t temp = 0;
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
-  const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
-  auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
-  return 2 * up(n * 4) + up(n) + up(blocks * kSegWords * 2) + up(temp);
+  return temp;
+}
+}  // namespace
+
+size_t parse_scratch_bytes(uint64_t n, uint64_t items_cap) {
+  return ParseLayout(n, items_cap, scan_temp_bytes(n)).end;
 }
 
 hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, hipStream_t stream) {
   const uint64_t n = a.n;
   const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
-  auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
+  const ParseLayout lay(n, a.items_cap, scan_temp_bytes(n));
+  if (lay.end > scratch_bytes) return hipErrorInvalidValue;
   char* s = (char*)scratch;
-  uint32_t* counts = (uint32_t*)s;
-  uint32_t* firsts = (uint32_t*)(s + up(n * 4));
-  uint8_t* modes = (uint8_t*)(s + 2 * up(n * 4));
-  uint16_t* pos_seg = (uint16_t*)(s + 2 * up(n * 4) + up(n));
-  const size_t fixed = 2 * up(n * 4) + up(n) + up(blocks * kSegWords * 2);
-  void* temp = s + fixed;
-  size_t temp_bytes = scratch_bytes - fixed;
+  uint32_t* counts = (uint32_t*)(s + lay.counts);
+  uint32_t* firsts = (uint32_t*)(s + lay.firsts);
+  uint8_t* modes = (uint8_t*)(s + lay.modes);
+  uint32_t* cursor = (uint32_t*)(s + lay.cursor);
+  uint32_t* bases = (uint32_t*)(s + lay.bases);
+  uint16_t* pos_seg = (uint16_t*)(s + lay.slots);
+  void* temp = s + lay.temp;
+  size_t temp_bytes = lay.end - lay.temp;
+  hipError_t e = hipMemsetAsync(cursor, 0, 4, stream);
+  if (e != hipSuccess) return e;
   parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
-                                                                    modes, pos_seg);
-  hipError_t e = hipGetLastError();
+                                                                    modes, pos_seg, cursor, bases, lay.seg_cap);
+  e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
   if (e != hipSuccess) return e;
   parse_emit_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
-                                                                    firsts, modes, pos_seg, a.items, a.items_cap,
+                                                                    firsts, modes, pos_seg, bases, a.items, a.items_cap,
                                                                     a.items_used);
   return hipGetLastError();
 }

@@ -20,8 +20,11 @@ struct ParseArgs {
   uint64_t* items_used;    // device word, nullable
 };
 
-// Device scratch of a parse of n frames (item counts, first indices, scan temporaries).
-size_t parse_scratch_bytes(uint64_t n);
+// Device scratch of a parse of n frames with room for at most items_cap items (item counts, first
+// indices, modes, scan temporaries, and header slots for min(64 n, items_cap) datagrams: the walk's
+// workgroups take their slot segments from a bump counter, and a workgroup that finds no room left
+// leaves its frames to the emit step's re-walk).
+size_t parse_scratch_bytes(uint64_t n, uint64_t items_cap);
 hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, hipStream_t stream);
 
 }  // namespace ufc_dev

@@ -1064,7 +1064,7 @@ int ufc_parse_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t*
   if (!d_bytes || !d_offsets || !d_valid || !d_infos || n >= ((size_t)1 << 31)) return UFC_ERR_INVALID_ARG;
   DeviceGuard g(ctx->device);
   hipError_t e;
-  const size_t need = ufc_dev::parse_scratch_bytes(n);
+  const size_t need = ufc_dev::parse_scratch_bytes(n, d_items ? (uint64_t)items_cap : 0);
   void* scratch = nullptr;  // this stream's own scratch (grows on the first or a larger batch only)
   if ((e = stream_scratch(ctx, kScratchParse, (hipStream_t)stream, need, &scratch)) != hipSuccess)
     return hip_fail(ctx, e);
