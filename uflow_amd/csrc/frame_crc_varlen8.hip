@@ -906,9 +906,10 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_stream8_kernel(const Ker
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 
-  // rounds of NS steps while anything is loaded, in flight or pending
+  // rounds of NS steps while anything is to be loaded or in flight (a frame still pending when
+  // every stream is drained is finished after the loop: nothing inside it would finish it)
   auto busy = [&]() -> bool {
-    bool b = !ldone || (pinfo & kRiLive);
+    bool b = !ldone;
 #pragma unroll
     for (int i = 0; i < NS; i++) b = b || (RI[i] & kRiLive);
     return __builtin_amdgcn_ballot_w64(b) != 0;
