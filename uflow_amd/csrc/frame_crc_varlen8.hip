@@ -583,7 +583,8 @@ UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(fal
 //     group_lin8) runs for all groups at once when every group has a pending frame or one must push
 //     a second: about one finish round per four steps instead of one whenever any group ends.
 //   * Frames the fast path cannot take (shorter than 4 bytes, ending past offsets[n] after rounding,
-//     windows 2 GB past the wave's base, longer than 32 MB) run byte-wise in the same loop.
+//     windows starting before the buffer or 2 GB past the wave's base, longer than 32 MB) run
+//     byte-wise in the same loop.
 namespace {
 
 constexpr uint32_t kStrOob = 0x80000000u;
@@ -656,7 +657,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_stream8_kernel(const Ker
     const uint64_t P = (len + t + 4 + 127) >> 7;
     const uint32_t pad = (uint32_t)(P * 128 - len - t);
     const uint64_t wend64 = E + t - wbase;
-    const bool slow = len < 4 || len > kStrMaxLen || E + t > offn || wend64 >= kStrLimit;
+    // (a window starting before the buffer: its lane that straddles byte 0 would load nothing)
+    const bool slow = len < 4 || len > kStrMaxLen || E + t > offn || wend64 >= kStrLimit || S < (uint64_t)pad;
     wend = slow ? 0u : (uint32_t)wend64;
     return slow ? (kSgSlow | (len >= 5 ? kSgLen5 : 0u))
                 : (pad | (t << 8) | (len >= 5 ? kSgLen5 : 0u) | ((uint32_t)P << 13));
