@@ -573,18 +573,18 @@ def test_tuning_only_modes_rejected(engine):
     from uflow_amd import _native as N
     for opt, val in ((N.UFC_OPT_FIXED_KERNEL, N.UFC_FIXED_CLAIM16), (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_SORTED),
                      (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_BLOCKED8), (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_CLAIM16),
-                     (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_BLOCKSTREAM)):
+                     (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_BLOCKSTREAM), (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_STREAM)):
         assert N.lib().ufc_ctx_set_option(engine._ctx, opt, val) == N.UFC_ERR_INVALID_ARG
         assert engine.get_option(opt) == 0
 
 
-@pytest.mark.parametrize("mode", ["generic", "sorted8", "stream"])
+@pytest.mark.parametrize("mode", ["generic", "sorted8"])
 def test_varlen_alternate_modes(engine, mode):
-    """The varlen kernel's product modes (ufc_ctx_set_option): the generic kernel, the 8-lane
-    sorted-runs kernel and the byte-balanced streaming kernel -- mixed lengths, edge lengths, seal,
-    gapped pairs (pairs always run the 8-lane kernel)."""
+    """The varlen kernel's product modes (ufc_ctx_set_option): the generic kernel and the 8-lane
+    sorted-runs kernel (the default, set explicitly) -- mixed lengths, edge lengths, seal, gapped
+    pairs (pairs run the 8-lane kernel under either)."""
     from uflow_amd import _native as N
-    value = {"generic": N.UFC_VARLEN_GENERIC, "sorted8": N.UFC_VARLEN_SORTED8, "stream": N.UFC_VARLEN_STREAM}[mode]
+    value = {"generic": N.UFC_VARLEN_GENERIC, "sorted8": N.UFC_VARLEN_SORTED8}[mode]
     engine.set_option(N.UFC_OPT_VARLEN_KERNEL, value)
     try:
         assert engine.get_option(N.UFC_OPT_VARLEN_KERNEL) == value

@@ -106,7 +106,9 @@ def varlen(eng, dev, reps, n=10_000_000):
     from uflow_amd import _native as N
     other = N.UFC_VARLEN_SORTED8 if eng.get_option(N.UFC_OPT_VARLEN_KERNEL) in (N.UFC_VARLEN_STREAM,) else N.UFC_VARLEN_STREAM
     saved = eng.get_option(N.UFC_OPT_VARLEN_KERNEL)
-    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, other)
+    if N.lib().ufc_ctx_set_option(eng._ctx, N.UFC_OPT_VARLEN_KERNEL, other) != N.UFC_OK:
+        other = N.UFC_VARLEN_GENERIC  # (the streaming kernel: tuning builds only)
+        eng.set_option(N.UFC_OPT_VARLEN_KERNEL, other)
     crc2 = torch.empty(n, dtype=torch.int32, device=dev)
     valid2 = torch.empty(n, dtype=torch.uint8, device=dev)
     fn2 = lambda: eng.crc_varlen(data, offsets, crc_out=crc2, valid_out=valid2)  # noqa: E731
@@ -116,7 +118,8 @@ def varlen(eng, dev, reps, n=10_000_000):
     settle(fn2)
     med2, _ = timed(fn2, reps)
     eng.set_option(N.UFC_OPT_VARLEN_KERNEL, saved)
-    ab = {"other_kernel": "stream" if other == N.UFC_VARLEN_STREAM else "sorted8", "other_kernel_ms": round(med2, 4),
+    ab = {"other_kernel": {N.UFC_VARLEN_STREAM: "stream", N.UFC_VARLEN_SORTED8: "sorted8"}.get(other, "generic"),
+          "other_kernel_ms": round(med2, 4),
           "other_equal_results": same}
     if not CHECK:
         return rates("3: varlen 10M x U[64,1500] device-resident (unchecked counter pass)", total, algo, med, mean,

@@ -886,7 +886,11 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_stream8_kernel(const Ker
     if (__builtin_amdgcn_ballot_w64(fast && (info & kRiG1)) != 0 && (info & kRiG1))
       x = fix_piece(L.lds, x, (int)pad - 128 - (int)(16u * c));
     Chains nv = V;
+#if defined(UFC_TUNING) && defined(UFC_STR_ABL) && (UFC_STR_ABL & 1)  // A/B: loads + control only
+    nv.v0 ^= x.x; nv.v1 ^= x.y; nv.v2 ^= x.z; nv.v3 ^= x.w;
+#else
     chain4(L, nv, x);
+#endif
     if (fast) {
       V.v0 = first ? fx.x : nv.v0;
       V.v1 = first ? fx.y : nv.v1;
@@ -928,12 +932,21 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_stream8_kernel(const Ker
   if (rem) store8(f_lo + done_cnt - rem, rem);
 }
 
+// Measured slower than the 8-lane set kernel on config 3 (2.82 against 1.55 ms, the same box; its
+// loads + control alone, without the CRC steps, take 2.39 ms: DESIGN.md section 5.2): tuning builds only.
+#ifdef UFC_TUNING
 #define UFC_STR_INST(SEAL) template __global__ void frame_crc_stream8_kernel<SEAL, 12>(const KernelParams);
 UFC_STR_INST(false) UFC_STR_INST(true)
 #undef UFC_STR_INST
+#endif
 
 const void* stream8_kernel_symbol(bool seal) {
+#ifdef UFC_TUNING
   return seal ? (const void*)frame_crc_stream8_kernel<true, 12> : (const void*)frame_crc_stream8_kernel<false, 12>;
+#else
+  (void)seal;
+  return nullptr;
+#endif
 }
 
 const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort) {

@@ -522,8 +522,7 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
     case UFC_OPT_VARLEN_KERNEL:
       if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_STREAM) return UFC_ERR_INVALID_ARG;
 #ifndef UFC_TUNING
-      if (value != UFC_VARLEN_AUTO && value != UFC_VARLEN_GENERIC && value != UFC_VARLEN_SORTED8 &&
-          value != UFC_VARLEN_STREAM)
+      if (value != UFC_VARLEN_AUTO && value != UFC_VARLEN_GENERIC && value != UFC_VARLEN_SORTED8)
         return UFC_ERR_INVALID_ARG;  // (round-1 and block-stream kernels: A/B in tuning builds)
 #endif
       break;
