@@ -9,6 +9,7 @@
 The plan itself is checked in C (tests/c/c_abi_smoke.c) and executed over gloo (test_shard_gloo.py).
 """
 import json
+import re
 import os
 import socket
 import subprocess
@@ -101,11 +102,13 @@ def test_ranks_on_one_device(world):
            os.path.join(repo, "tests", "gpu_shard_worker.py")]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=repo)
     assert p.returncode == 0, p.stderr[-3000:]
-    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 2, p.stdout[-2000:]  # one line per root (last rank: fixed; rank 0: varlen)
+    # one JSON object per root (last rank: fixed; rank 0: varlen); the two processes share the pipe,
+    # so their lines may arrive on one line
+    objs = re.findall(r"\{[^{}]*\}", p.stdout)
+    assert len(objs) == 2, p.stdout[-2000:]
     j = {}
-    for ln in lines:
-        j.update(json.loads(ln))
+    for o in objs:
+        j.update(json.loads(o))
     assert j["world"] == world
     assert j["fixed_crc_ok"] and j["fixed_valid_ok"] and j["fixed_invalid"] == len(range(0, 9_000_001, 1013))
     assert j["varlen_crc_ok"] and j["varlen_valid_ok"] and j["varlen_invalid"] == len(range(0, 1_500_001, 7))

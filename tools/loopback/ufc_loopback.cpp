@@ -523,11 +523,17 @@ int run_stream_inline(const Args& a) {
   const int TX = R * std::max(1, a.tx_per_rx);
   const double rate_tx = a.rate_gbps > 0 ? a.rate_gbps * 1e9 / TX : 0.0;  // B/s per sender
   std::atomic<uint64_t> sent_total{0};
-  const double t_send0 = now_s();  // (pacing clock and the sender-clock goodput start)
+  // Senders start once every receiver is ready (GPU context, pinned buffers and the staging warm-up
+  // take a fresh process up to seconds, which unstarted receivers would otherwise lose as datagrams).
+  std::atomic<int> rx_ready{0};
+  std::atomic<double> t_send0{0.0};  // (pacing clock and the sender-clock goodput start)
   std::vector<double> t_send_end(TX, 0.0);
   for (int t = 0; t < TX; t++) {
     // sender t: frames [F t / TX, F (t+1) / TX) to port + t % R
     threads.emplace_back([&, t] {
+      while (rx_ready.load() < R) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      if (t == 0) t_send0.store(now_s());
+      while (t_send0.load() == 0.0) std::this_thread::yield();
       const int tx = udp_socket(0, false, 0);
       const sockaddr_in to = loopback((uint16_t)(a.port + t % R));
       const uint64_t lo = a.frames * t / TX, hi = a.frames * (t + 1) / TX;
@@ -537,7 +543,7 @@ int run_stream_inline(const Args& a) {
       std::vector<uint8_t> scratch((size_t)M * kFrame);
       for (uint64_t s = lo; s < hi;) {
         const int m = (int)std::min<uint64_t>(M, hi - s);
-        pace(t_send0, (double)(s - lo) * kFrame, rate_tx);
+        pace(t_send0.load(), (double)(s - lo) * kFrame, rate_tx);
         for (int i = 0; i < m; i++) {
           const uint64_t q = s + i;
           uint8_t* f = ring.data() + (size_t)(q % kRing) * kFrame;
@@ -578,9 +584,12 @@ int run_stream_inline(const Args& a) {
         uint8_t* valid = nullptr;
         size_t n = 0;
       } bufs[2];
+      bool counted = false;
       auto fail = [&](const char* what) {
         fprintf(stderr, "receiver %d: %s\n", r, what);
         failed++;
+        if (!counted) rx_ready++;  // (never leave the senders waiting)
+        counted = true;
       };
       if (a.gpu) {
         if (ufc_ctx_create(&ctx, 0) != UFC_OK) return fail("ufc_ctx_create");
@@ -612,6 +621,8 @@ int run_stream_inline(const Args& a) {
       std::vector<ufc_item> items(UFC_DATA_FRAME_MAX_DATAGRAM_COUNT);
       std::vector<mmsghdr> msgs(B);
       std::vector<iovec> iov(B);
+      rx_ready++;
+      counted = true;
       // parse + payload check of a gated batch (the rest of Frame::read and the application)
       auto handle = [&](const Buf& b) {
         for (size_t i = 0; i < b.n; i++) {
@@ -735,12 +746,13 @@ int run_stream_inline(const Args& a) {
     gate_max = std::max(gate_max, S.t_gate);
   }
   const double span = std::max(T.t_last - T.t_first, 1e-9);
-  double send_end = t_send0;
+  const double t_start = t_send0.load();
+  double send_end = t_start;
   for (double t : t_send_end) send_end = std::max(send_end, t);
   const uint64_t sent = sent_total.load();
   // Goodput on the senders' clock: frame bytes received / (last datagram received - first sent):
   // comparable between gates whatever each one dropped (ideal_transfer.rs).
-  const double span_tx = std::max((T.received ? T.t_last : send_end) - t_send0, 1e-9);
+  const double span_tx = std::max((T.received ? T.t_last : send_end) - t_start, 1e-9);
   printf("{\"config\": \"5: ideal_transfer-style loopback, inline receive loops (receive + %s gate + "
          "parse + payload check per thread)\", \"rx_threads\": %d, \"frame_bytes\": %zu, \"sent\": %llu, "
          "\"received\": %llu, \"lost\": %llu, \"loss_frac\": %.5f, \"offered_GB_s\": %.3f, "
@@ -755,7 +767,7 @@ int run_stream_inline(const Args& a) {
          (unsigned long long)(sent - std::min(sent, T.received)), sent ? 1.0 - (double)T.received / (double)sent : 0.0,
          a.rate_gbps, (unsigned long long)T.valid,
          (unsigned long long)T.invalid, (unsigned long long)T.parsed, (unsigned long long)T.payload_bad, span,
-         T.received / span, T.bytes / span / 1e9, T.bytes / span_tx / 1e9, send_end - t_send0, T.t_gate,
+         T.received / span, T.bytes / span / 1e9, T.bytes / span_tx / 1e9, send_end - t_start, T.t_gate,
          T.t_gate / (span * R), T.t_recv, T.t_sync, T.t_handle, a.batch, failed.load(), TX, rcvbuf);
   return (T.payload_bad == 0 && T.received > 0 && failed.load() == 0) ? 0 : 1;
 }

@@ -177,8 +177,11 @@ struct Buf8 {
 // WAVES waves per workgroup (one workgroup per CU); DEPTH sets per wave in the ring (the set
 // computed plus DEPTH - 1 in flight).  p.offsets = the run-sorted records, p.offsets_csr = the
 // CSR offsets (nullptr for pairs: p.frame_len = the buffer length, relative offsets < 2^31).
-template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT>
+// SORTW: runs are ordered by block count within aligned windows of SORTW frames (64: the whole run;
+// 8: no reordering across sets, i.e. each set is 8 consecutive frames).
+template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
+  static_assert(SORTW == 8 || SORTW == 16 || SORTW == 32 || SORTW == 64, "sort window");
   constexpr int JM = kV8Blocks;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
 #ifdef UFC_TUNING
@@ -229,15 +232,23 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     const uint64_t n4 = len >= 4 ? len - 4 : len;
     const uint64_t J = (n4 + 8 + 255) >> 8;
     const uint32_t key = !live ? 8u : ((len >= 4 && len < 0x40000000ull && J <= (uint64_t)JM) ? (uint32_t)J : 7u);
+    if constexpr (SORTW == 8) {  // sets of consecutive frames: no reordering
+      out.a_lo = (uint32_t)a;
+      out.a_hi = (uint32_t)(a >> 32);
+      out.len = (uint32_t)min(len, (uint64_t)0xFFFFFFFFu);
+      out.info = L.lane | (live ? 0u : 0x80000000u);
+      return;
+    }
+    const uint64_t qmask = SORTW == 64 ? ~0ull : (((1ull << SORTW) - 1ull) << (L.lane & ~(uint32_t)(SORTW - 1)));
     uint32_t below = 0, rank_in = 0;
 #pragma unroll
     for (uint32_t k = 1; k <= 8; k++) {
-      const uint64_t m = __builtin_amdgcn_ballot_w64(key == k);
+      const uint64_t m = __builtin_amdgcn_ballot_w64(key == k) & qmask;
       below += (k < key) ? (uint32_t)__builtin_popcountll(m) : 0u;
       const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       rank_in = (k == key) ? rk : rank_in;
     }
-    const int dst = (int)((below + rank_in) * 4u);
+    const int dst = (int)(((L.lane & ~(uint32_t)(SORTW - 1)) + below + rank_in) * 4u);
     out.a_lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)a);
     out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(a >> 32));
     out.len = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)min(len, (uint64_t)0xFFFFFFFFu));
@@ -343,7 +354,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       for (int h = 0; h < 2; h++) {
         uint32_t vo = base;
         if (j == 0) vo = (128u * h + 16u * L.col + 16u <= pad) ? kV8Oob : vo;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, kV8Aux);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, AUX);
         b.x[2 * j + h] = make_uint4(v.x, v.y, v.z, v.w);
       }
     }
@@ -556,14 +567,22 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 
 #define UFC_V8_INST(SEAL, PAIRS, IS) \
   template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, 12, 2, IS>(const KernelParams);
+#define UFC_V8_INSTW(SEAL, SW) \
+  template __global__ void frame_crc_varlen8_kernel<SEAL, false, 12, 2, true, SW>(const KernelParams);
+#define UFC_V8_INSTA(SW) \
+  template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, SW, 2>(const KernelParams);
 // Product: 12 waves, 2 sets per wave in the ring (three waves per SIMD; config 3 1.69 ms kernel
 // against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill), runs sorted
 // in the kernel.  The pre-sorted variant (records from sort_runs) is kept for A/B in tuning builds.
 UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
 #ifdef UFC_TUNING
 UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
+UFC_V8_INSTW(false, 8) UFC_V8_INSTW(false, 16) UFC_V8_INSTW(false, 32) UFC_V8_INSTW(true, 8) UFC_V8_INSTW(true, 16)
+UFC_V8_INSTW(true, 32) UFC_V8_INSTA(8) UFC_V8_INSTA(16) UFC_V8_INSTA(32) UFC_V8_INSTA(64)
 #endif
 #undef UFC_V8_INST
+#undef UFC_V8_INSTW
+#undef UFC_V8_INSTA
 
 // =============================================================================================
 // Byte-balanced streaming kernel (round 3, SURVEY.md section 7 step 6: "one byte stream"): CSR
@@ -585,6 +604,7 @@ UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(fal
 //   * Frames the fast path cannot take (shorter than 4 bytes, ending past offsets[n] after rounding,
 //     windows starting before the buffer or 2 GB past the wave's base, longer than 32 MB) run
 //     byte-wise in the same loop.
+#ifdef UFC_TUNING
 namespace {
 
 constexpr uint32_t kStrOob = 0x80000000u;
@@ -934,7 +954,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_stream8_kernel(const Ker
 
 // Measured slower than the 8-lane set kernel on config 3 (2.82 against 1.55 ms, the same box; its
 // loads + control alone, without the CRC steps, take 2.39 ms: DESIGN.md section 5.2): tuning builds only.
-#ifdef UFC_TUNING
 #define UFC_STR_INST(SEAL) template __global__ void frame_crc_stream8_kernel<SEAL, 12>(const KernelParams);
 UFC_STR_INST(false) UFC_STR_INST(true)
 #undef UFC_STR_INST
@@ -949,7 +968,32 @@ const void* stream8_kernel_symbol(bool seal) {
 #endif
 }
 
-const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort) {
+const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux) {
+#ifdef UFC_TUNING
+  if (insort && !pairs && !seal && aux == 2) {  // A/B: non-temporal loads (CSR validate)
+    switch (sortw) {
+      case 8: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 8, 2>;
+      case 16: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 16, 2>;
+      case 32: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 32, 2>;
+      case 64: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, 2>;
+      default: return nullptr;
+    }
+  }
+  if (aux != kV8Aux) return nullptr;
+  if (insort && !pairs && sortw != 64) {  // A/B: narrower sort windows (CSR)
+    switch (sortw) {
+      case 8: return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 8>
+                          : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 8>;
+      case 16: return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 16>
+                           : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 16>;
+      case 32: return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 32>
+                           : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 32>;
+      default: return nullptr;
+    }
+  }
+#else
+  if (sortw != 64 || aux != kV8Aux) return nullptr;
+#endif
   if (insort) {
     if (pairs)
       return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true>

@@ -333,7 +333,12 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   if (const char* ps = std::getenv("UFC_V8_PRESORT")) insort = std::atoi(ps) == 0;
 #endif
   const int waves = 12;
-  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, insort);
+  int sortw = 64, aux = 0;  // runs sorted whole, default-policy loads; UFC_V8_SORTW / UFC_V8_AUX (tuning): A/B
+#ifdef UFC_TUNING
+  if (const char* sw = std::getenv("UFC_V8_SORTW")) sortw = std::atoi(sw);
+  if (const char* ax = std::getenv("UFC_V8_AUX")) aux = std::atoi(ax);
+#endif
+  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, insort, sortw, aux);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain128;
   kp.nib_img = ctx->d_nib32;
