@@ -106,10 +106,7 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 #define UFC_OPT_SEAL_KERNEL 3    /* fixed-stride seals: */
 #define UFC_SEAL_TWO_PASS 0      /*   validate kernel's CRC words, then a non-temporal trailer pass (default) */
 #define UFC_SEAL_INLINE 1        /*   trailers written by the CRC kernel itself (round-1/2 default) */
-#define UFC_OPT_PARSE_KERNEL 4   /* ufc_parse_batch_varlen (uflow_frame_codec.h): */
-#define UFC_PARSE_ONE_PASS 0     /*   tiles staged in LDS, walked, scanned (decoupled look-back), emitted (default) */
-#define UFC_PARSE_THREE_PASS 1   /*   walk / scan / emit kernels over global memory (round-2 default) */
-#define UFC_OPT_COUNT_ 5
+#define UFC_OPT_COUNT_ 4
 int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value);
 int ufc_ctx_get_option(const ufc_ctx* ctx, int option);
 

@@ -234,16 +234,6 @@ def test_varlen_misaligned_base(engine, shift):
 
 # ---- batched Frame::read past the CRC gate (frame_parse.hip) ----
 
-@pytest.fixture(params=["one_pass", "three_pass"])
-def parse_kernel(request, engine):
-    """Both batch-parse kernels (UFC_OPT_PARSE_KERNEL): the one-pass tile kernel (default) and the
-    three-pass walk / scan / emit shape."""
-    from uflow_amd import _native as NN
-    engine.set_option(NN.UFC_OPT_PARSE_KERNEL,
-                      NN.UFC_PARSE_ONE_PASS if request.param == "one_pass" else NN.UFC_PARSE_THREE_PASS)
-    yield request.param
-    engine.set_option(NN.UFC_OPT_PARSE_KERNEL, NN.UFC_PARSE_THREE_PASS)
-
 def _codec_batch(rng_seed, n):
     import random
     from oracle import codec as C
@@ -274,7 +264,7 @@ def _codec_batch(rng_seed, n):
     return frames, np.frombuffer(b"".join(frames), dtype=np.uint8).copy(), offsets
 
 
-def test_parse_varlen_vs_oracle(engine, parse_kernel):
+def test_parse_varlen_vs_oracle(engine):
     """GPU gate + GPU parse vs the Python codec oracle, frame by frame."""
     from oracle import codec as C
     from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE
@@ -341,7 +331,7 @@ def _parse_edge_batch(seed):
     return frames, np.frombuffer(b"".join(frames), dtype=np.uint8).copy(), offsets
 
 
-def test_parse_varlen_slow_paths_and_cap(engine, parse_kernel):
+def test_parse_varlen_slow_paths_and_cap(engine):
     """Every parse path vs the codec oracle, then the same batch with an item cap that cuts
     through the middle (items past the cap are not written; item_first / items_used unchanged)."""
     from oracle import codec as C
@@ -386,7 +376,7 @@ def test_parse_varlen_slow_paths_and_cap(engine, parse_kernel):
     assert (got[cap:] == 0xA5).all()
 
 
-def test_parse_varlen_vs_host_parse_large(engine, parse_kernel):
+def test_parse_varlen_vs_host_parse_large(engine):
     """A 200k-frame batch: device parse == host parse (itself pinned to the oracle on CPU)."""
     from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host
     frames, data, offsets = _codec_batch(10, 600)
@@ -622,7 +612,7 @@ def test_fixed_alternate_modes(engine, mode):
         engine.set_option(N.UFC_OPT_FIXED_KERNEL, N.UFC_FIXED_AUTO)
 
 
-def test_parse_two_streams(engine, parse_kernel):
+def test_parse_two_streams(engine):
     """Two batch parses queued on different streams of one context at once: each stream has its own
     scan scratch, so both results equal the single-stream parse."""
     frames, data, offsets = _codec_batch(11, 2000)

@@ -46,8 +46,7 @@ def test_constants_match_header():
     assert int(consts["UFC_MAX_FRAME_SIZE"]) == crc.MAX_FRAME_SIZE == 1472
     assert int(consts["UFC_OK"]) == _native.UFC_OK == 0
     for name in ("UFC_OPT_FIXED_KERNEL", "UFC_OPT_VARLEN_KERNEL", "UFC_OPT_GENERIC_JC", "UFC_OPT_SEAL_KERNEL",
-                 "UFC_FIXED_CLAIM16", "UFC_VARLEN_SORTED8", "UFC_VARLEN_STREAM", "UFC_SEAL_TWO_PASS", "UFC_SEAL_INLINE",
-                 "UFC_OPT_PARSE_KERNEL", "UFC_PARSE_ONE_PASS", "UFC_PARSE_THREE_PASS"):
+                 "UFC_FIXED_CLAIM16", "UFC_VARLEN_SORTED8", "UFC_VARLEN_STREAM", "UFC_SEAL_TWO_PASS", "UFC_SEAL_INLINE"):
         assert int(consts[name]) == getattr(_native, name), name
 
 

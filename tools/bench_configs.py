@@ -30,7 +30,6 @@ import torch  # noqa: E402
 
 import oracle  # noqa: E402  (the checker and the CPU baseline only)
 from uflow_amd import synth  # noqa: E402
-from uflow_amd import _native as N  # noqa: E402
 from uflow_amd.batch import FrameCrcEngine  # noqa: E402
 
 PEAK = 8e12
@@ -229,27 +228,16 @@ def parse(eng, dev, reps, n=1_000_000):
     d = torch.from_numpy(data).to(dev)
     o = torch.from_numpy(offsets).to(dev)
     _, valid = eng.crc_varlen(d, o)
-    res = {}
-    outs = {}
-    for name, kern in (("one_pass", N.UFC_PARSE_ONE_PASS), ("three_pass", N.UFC_PARSE_THREE_PASS)):
-        eng.set_option(N.UFC_OPT_PARSE_KERNEL, kern)
-        infos, items, used = eng.parse_varlen(d, o, valid)
-        torch.cuda.synchronize()
-        k = int(used.cpu()[0])
-        outs[name] = (infos.cpu(), items[:k].cpu(), k)
-        cap = items.shape[0]
-        fn = lambda: eng.parse_varlen(d, o, valid, items_cap=cap)  # noqa: E731
-        settle(fn)
-        res[name] = timed(fn, reps)
-    eng.set_option(N.UFC_OPT_PARSE_KERNEL, N.UFC_PARSE_THREE_PASS)
-    a, b = outs["one_pass"], outs["three_pass"]
-    same = a[2] == b[2] and torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
-    med, mean = res["one_pass"]
+    infos, items, used = eng.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    cap = items.shape[0]
+    fn = lambda: eng.parse_varlen(d, o, valid, items_cap=cap)  # noqa: E731
+    settle(fn)
+    med, mean = timed(fn, reps)
     total = int(offsets[-1])
-    return {"config": "f3: device parse of 1M uflow frames after the gate (one-pass tile kernel; the three-pass "
-                      "walk / scan / emit shape timed beside it)", "frames": n,
-            "frame_bytes": total, "items": a[2], "ms": round(med, 4), "mean_ms": round(mean, 4),
-            "three_pass_ms": round(res["three_pass"][0], 4), "outputs_identical": bool(same),
+    k = int(used.cpu()[0])
+    return {"config": "f3: device parse (count, scan, fill) of 1M uflow frames after the gate", "frames": n,
+            "frame_bytes": total, "items": k, "ms": round(med, 4), "mean_ms": round(mean, 4),
             "frames_per_s": round(n / med * 1e3), "GB_s_of_frame_bytes": round(total / med / 1e-3 / 1e9, 1)}
 
 

@@ -298,9 +298,6 @@ constexpr int kLeanAblCompute = 2;
 __device__ __forceinline__ void st_u32_hidden(uint32_t* a, uint32_t v) {
   asm volatile("global_store_dword %0, %1, off" : : "v"(a), "v"(v));
 }
-__device__ __forceinline__ void st_u32_hidden_nt(uint32_t* a, uint32_t v) {  // non-temporal
-  asm volatile("global_store_dword %0, %1, off nt" : : "v"(a), "v"(v));
-}
 __device__ __forceinline__ void st_u8_hidden(uint8_t* a, uint32_t v) {
   asm volatile("global_store_byte %0, %1, off" : : "v"(a), "v"(v));
 }

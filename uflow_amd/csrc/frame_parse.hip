@@ -244,239 +244,6 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
   }
 }
 
-// =============================================================================================
-// One-pass parse (the default): tiles of kFuseFrames consecutive frames, claimed in order from a
-// ticket counter by workgroups of 256 threads (three per CU).  Per tile:
-//   1. stage: the tile's bytes [offsets[f0], offsets[f0 + T]) are copied into LDS with coalesced
-//      16-byte loads, up to kFuseData bytes (a frame not wholly inside the staged window is read
-//      from global memory instead, byte by byte, as the three-pass walk does);
-//   2. walk: one thread per frame runs the same read_frame_to as the host codec over the staged
-//      bytes (LDS latency instead of an HBM round trip per datagram), recording each datagram
-//      header's frame offset in LDS slots;
-//   3. scan + decoupled look-back: the tile's item count is published (flag 1) at once, the global
-//      first item found by walking back over the predecessors' published counts / prefixes, and
-//      the tile's inclusive prefix published (flag 2); tiles are claimed in order, so every
-//      predecessor belongs to a running workgroup;
-//   4. emit: item-parallel over the tile, headers decoded from LDS, 24-byte records stored
-//      consecutively; infos written once with item_first.  Frames with more than kPosSlots
-//      datagrams or over 64 KiB are walked again from global memory by their own thread.
-// Every byte of the batch is read once, coalesced, instead of the three-pass shape's two
-// dependent-load walks over ~every line (walk + emit: 1.3 GB of scattered reads for 1.41 GB).
-constexpr int kFuseThreads = 256;
-constexpr int kFuseFrames = 32;              // frames per tile
-constexpr uint32_t kFuseData = 46u * 1024u;  // staged bytes per tile (uflow frames: <= 1472 B)
-constexpr uint32_t kFuseSpin = 1u << 22;     // look-back wait bound (s_sleep steps; never reached)
-constexpr uint64_t kFlagAgg = 1ull << 62, kFlagIncl = 2ull << 62, kFlagMask = 3ull << 62;
-
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(3))) uint8_t l_u8;
-typedef const __attribute__((address_space(3))) uint32_t l_u32;
-
-struct LdsBytes {
-  l_u8* p;
-  __device__ uint32_t operator()(uint32_t i) const { return p[i]; }
-};
-
-// Walk sink: header offsets into LDS slots (slot k of tile frame f at k * kFuseFrames + f).
-struct TilePosSink {
-  static constexpr bool kDecode = false;
-  uint16_t* slot;
-  __device__ bool on() const { return true; }
-  __device__ void operator()(uint32_t, const ufc_item&) const {}
-  __device__ void header(uint32_t k, uint32_t off) const { slot[k * kFuseFrames] = (uint16_t)off; }
-};
-
-struct FuseLds {
-  uint4 data[kFuseData / 16];
-  uint16_t slots[kPosSlots * kFuseFrames];
-  uint64_t off[kFuseFrames + 1];
-  uint32_t first[kFuseFrames];
-  uint8_t mode[kFuseFrames];
-  uint8_t inlds[kFuseFrames];
-  uint32_t tile;
-  uint32_t agg;
-  uint64_t excl;
-};
-static_assert(sizeof(FuseLds) * 3 <= 160 * 1024, "three workgroups per CU");
-
-__global__ __launch_bounds__(kFuseThreads) void parse_fused_kernel(const uint8_t* bytes, const uint64_t* offsets,
-                                                                   uint64_t n, const uint8_t* valid,
-                                                                   ufc_frame_info* infos, ufc_item* items,
-                                                                   uint64_t cap, uint64_t* items_used,
-                                                                   uint32_t* ticket, uint64_t* state,
-                                                                   uint32_t* err) {
-  __shared__ FuseLds L;
-  const uint32_t t = threadIdx.x;
-  const uint64_t ntiles = (n + kFuseFrames - 1) / kFuseFrames;
-  l_u8* const dl = (l_u8*)(const uint8_t*)L.data;
-  for (;;) {
-    if (t == 0) L.tile = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t tile = L.tile;
-    if ((uint64_t)tile >= ntiles) break;
-    const uint64_t f0 = (uint64_t)tile * kFuseFrames;
-    const uint32_t nb = (uint32_t)min((uint64_t)kFuseFrames, n - f0);
-    if (t <= nb) L.off[t] = offsets[f0 + t];
-    __syncthreads();
-
-    // ---- 1. stage the tile's bytes (16-byte chunks from the aligned chunk of its first byte) ----
-    const uint64_t a0 = L.off[0], an = L.off[nb];
-    const uintptr_t s_addr = (uintptr_t)(bytes + a0);
-    const uint32_t delta = (uint32_t)(s_addr & 15u);
-    const uint64_t span = an >= a0 ? an - a0 : 0;
-    const uint32_t staged = (uint32_t)min(span + delta, (uint64_t)kFuseData);  // bytes held, from the chunk start
-    {  // every load issued before the first LDS write (chunks past the staged bytes: out of range, no request)
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(s_addr - delta), 0, (int)staged, 0x00020000);
-      const uint32_t nch = (staged + 15u) >> 4;
-      constexpr int kPer = (kFuseData / 16 + kFuseThreads - 1) / kFuseThreads;
-      u32x4v v[kPer];
-#pragma unroll
-      for (int k = 0; k < kPer; k++) {
-        const uint32_t i = t + kFuseThreads * k;
-        v[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i < nch ? 16u * i : 0x80000000u), 0, 2);
-      }
-#pragma unroll
-      for (int k = 0; k < kPer; k++) {
-        const uint32_t i = t + kFuseThreads * k;
-        if (i < nch) L.data[i] = make_uint4(v[k].x, v[k].y, v[k].z, v[k].w);
-      }
-    }
-    __syncthreads();
-
-    // ---- 2. walk: one thread per frame ----
-    uint32_t cnt = 0;
-    uint8_t mode = kItemsNone;
-    ufc_frame_info info{};
-    if (t < nb) {
-      const uint64_t a = L.off[t], b = L.off[t + 1];
-      const uint64_t len64 = b >= a ? b - a : 0;
-      const uint32_t len = len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
-      const uint64_t rel = a - a0 + delta;
-      const bool in = a >= a0 && rel + len64 <= staged;
-      const bool crc_ok = valid[f0 + t] != 0;
-      const bool ok = in ? ufc_codec::read_frame_to(LdsBytes{dl + (uint32_t)rel}, len, crc_ok, info,
-                                                    TilePosSink{L.slots + t}, kPosSlots)
-                         : ufc_codec::read_frame_to(DevBytes{bytes + a}, len, crc_ok, info, TilePosSink{L.slots + t},
-                                                    kPosSlots);
-      cnt = ok ? info.item_count : 0u;
-      if (cnt) {
-        if (info.kind == UFC_FRAME_ACK)
-          mode = kItemsAck;
-        else if (cnt <= kPosSlots && len <= 0xFFFFu)
-          mode = kItemsPos;
-        else
-          mode = kItemsWalk;
-      }
-      L.mode[t] = mode;
-      L.inlds[t] = in ? 1 : 0;
-    }
-
-    // ---- 3. the tile's item scan (wave 0) and the decoupled look-back (thread 0) ----
-    if (t < 64) {
-      uint32_t x = t < nb ? cnt : 0u;
-#pragma unroll
-      for (int d = 1; d < kFuseFrames; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if ((int)(t & 63u) >= d) x += y;
-      }
-      if (t < kFuseFrames) L.first[t] = x - (t < nb ? cnt : 0u);  // exclusive
-      if (t == kFuseFrames - 1) {
-        const uint32_t agg = x;
-        L.agg = agg;
-        uint64_t excl = 0;
-        if (tile == 0) {
-          __hip_atomic_store(state + tile, kFlagIncl | (uint64_t)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        } else {
-          __hip_atomic_store(state + tile, kFlagAgg | (uint64_t)agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-          uint64_t j = tile;
-          uint32_t spins = 0;
-          while (j > 0) {
-            const uint64_t s = __hip_atomic_load(state + j - 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t fl = s & kFlagMask;
-            if (fl == 0) {
-              if (++spins > kFuseSpin) {  // (a predecessor that never publishes: flag it, do not hang)
-                atomicOr(err, 1u);
-                break;
-              }
-              __builtin_amdgcn_s_sleep(2);
-              continue;
-            }
-            excl += s & ~kFlagMask;
-            if (fl == kFlagIncl) break;
-            j--;
-          }
-          __hip_atomic_store(state + tile, kFlagIncl | (excl + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        L.excl = excl;
-        if (f0 + nb == n && items_used) *items_used = excl + agg;
-      }
-    }
-    __syncthreads();
-    const uint64_t excl = L.excl;
-    const uint32_t agg = L.agg;
-    if (t < nb) {
-      info.item_first = (uint32_t)(excl + L.first[t]);
-      infos[f0 + t] = info;
-    }
-
-    // ---- 4. emit ----
-    if (items) {
-      for (uint32_t q = t; q < agg && excl + q < cap; q += kFuseThreads) {
-        uint32_t lo = 0, hi = nb - 1;  // owner: the last frame whose first item is <= q
-        while (lo < hi) {
-          const uint32_t mid = (lo + hi + 1) >> 1;
-          if (L.first[mid] <= q)
-            lo = mid;
-          else
-            hi = mid - 1;
-        }
-        const uint32_t f = lo, k = q - L.first[f];
-        const uint8_t m = L.mode[f];
-        if (m != kItemsPos && m != kItemsAck) continue;
-        const uint32_t hoff = m == kItemsPos ? (uint32_t)L.slots[k * kFuseFrames + f]
-                                             : 1u + ufc_codec::kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
-        uint32_t w[4];
-        if (L.inlds[f]) {  // the header's 14 bytes from LDS: five aligned words, realigned
-          const uint32_t p = (uint32_t)(L.off[f] - a0) + delta + hoff;
-          const uint32_t al = p & ~3u, sh = p & 3u;
-          uint32_t x[5];
-#pragma unroll
-          for (int i = 0; i < 5; i++) x[i] = (al + 4u * i < kFuseData) ? *(l_u32*)(dl + al + 4u * i) : 0u;
-#pragma unroll
-          for (int i = 0; i < 4; i++) w[i] = __builtin_amdgcn_alignbyte(x[i + 1], x[i], sh);
-        } else {
-          const DevBytes rd{bytes + L.off[f] + hoff};
-#pragma unroll
-          for (int i = 0; i < 4; i++) w[i] = 0;
-          const uint32_t nbytes = m == kItemsAck ? UFC_ACK_GROUP_SIZE : 14u;
-          for (uint32_t c = 0; c < nbytes; c++) w[c >> 2] |= rd(c) << (8 * (c & 3));
-        }
-        auto h = [&](uint32_t c) -> uint32_t { return (w[c >> 2] >> (8 * (c & 3))) & 0xFFu; };
-        ufc_item it{};
-        if (m == kItemsPos) {
-          uint32_t hs, dlen;
-          ufc_codec::datagram_size(h, hs, dlen);
-          ufc_codec::decode_datagram(h, hs, it);
-          it.data_offset = hoff + hs;
-        } else {
-          ufc_codec::decode_ack_group(h, it);
-        }
-        store_item(items + excl + q, it);
-      }
-      // frames whose headers did not fit the slots: walked again, items stored directly
-      if (t < nb && mode == kItemsWalk && excl + L.first[t] < cap) {
-        const uint64_t g0 = excl + L.first[t];
-        const uint64_t a = L.off[t], b = L.off[t + 1];
-        const uint32_t len = (uint32_t)min(b - a, (uint64_t)0xFFFFFFFFu);
-        const uint32_t room = (uint32_t)min((uint64_t)cnt, cap - g0);
-        ufc_frame_info again;
-        ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[f0 + t] != 0, again, PackedSink{items + g0}, room);
-      }
-    }
-    __syncthreads();  // (LDS reused by the next tile)
-  }
-}
-
 }  // namespace
 
 namespace {
@@ -503,29 +270,12 @@ size_t scan_temp_bytes(uint64_t n) {
 }
 }  // namespace
 
-// One-pass parse scratch: ticket and error words, then one look-back word per tile.
-static uint64_t fused_scratch(uint64_t n) { return 256 + (n + kFuseFrames - 1) / kFuseFrames * 8; }
-
 size_t parse_scratch_bytes(uint64_t n, uint64_t items_cap) {
-  return std::max<uint64_t>(ParseLayout(n, items_cap, scan_temp_bytes(n)).end, fused_scratch(n));
+  return ParseLayout(n, items_cap, scan_temp_bytes(n)).end;
 }
 
 hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, hipStream_t stream) {
   const uint64_t n = a.n;
-  if (a.kernel == kParseFused) {
-    const uint64_t need = fused_scratch(n);
-    if (need > scratch_bytes) return hipErrorInvalidValue;
-    uint32_t* ticket = (uint32_t*)scratch;
-    uint32_t* err = ticket + 1;
-    uint64_t* state = (uint64_t*)((char*)scratch + 256);
-    hipError_t e = hipMemsetAsync(scratch, 0, need, stream);
-    if (e != hipSuccess) return e;
-    const uint64_t ntiles = (n + kFuseFrames - 1) / kFuseFrames;
-    const uint64_t grid = std::min<uint64_t>(ntiles, (uint64_t)std::max(1, a.ncu) * 3);
-    parse_fused_kernel<<<(unsigned)grid, kFuseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, a.items,
-                                                                   a.items_cap, a.items_used, ticket, state, err);
-    return hipGetLastError();
-  }
   const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
   const ParseLayout lay(n, a.items_cap, scan_temp_bytes(n));
   if (lay.end > scratch_bytes) return hipErrorInvalidValue;

@@ -18,10 +18,7 @@ struct ParseArgs {
   ufc_item* items;         // nullable
   uint64_t items_cap;
   uint64_t* items_used;    // device word, nullable
-  int kernel;              // kParseFused (one pass, default) or kParseThreePass (walk / scan / emit)
-  int ncu;                 // compute units (grid of the one-pass kernel)
 };
-constexpr int kParseFused = 0, kParseThreePass = 1;
 
 // Device scratch of a parse of n frames with room for at most items_cap items (item counts, first
 // indices, modes, scan temporaries, and header slots for min(64 n, items_cap) datagrams: the walk's

@@ -537,9 +537,6 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
     case UFC_OPT_SEAL_KERNEL:
       if (value < UFC_SEAL_TWO_PASS || value > UFC_SEAL_INLINE) return UFC_ERR_INVALID_ARG;
       break;
-    case UFC_OPT_PARSE_KERNEL:
-      if (value < UFC_PARSE_ONE_PASS || value > UFC_PARSE_THREE_PASS) return UFC_ERR_INVALID_ARG;
-      break;
     default: return UFC_ERR_INVALID_ARG;
   }
   ctx->opt[option] = value;
@@ -603,7 +600,6 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
   if (const char* k = std::getenv("UFC_SEAL_KERNEL"))
     ctx->opt[UFC_OPT_SEAL_KERNEL] = std::strcmp(k, "inline") == 0 ? UFC_SEAL_INLINE : UFC_SEAL_TWO_PASS;
 #endif
-  ctx->opt[UFC_OPT_PARSE_KERNEL] = UFC_PARSE_THREE_PASS;  // (until the one-pass kernel is GPU-validated)
   *out = ctx;
   return UFC_OK;
 }
@@ -1077,10 +1073,7 @@ int ufc_parse_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t*
   if ((e = stream_scratch(ctx, kScratchParse, (hipStream_t)stream, need, &scratch)) != hipSuccess)
     return hip_fail(ctx, e);
   ufc_dev::ParseArgs a{d_bytes, d_offsets, (uint64_t)n, d_valid, d_infos, d_items, (uint64_t)(d_items ? items_cap : 0),
-                       d_items_used,
-                       ctx->opt[UFC_OPT_PARSE_KERNEL] == UFC_PARSE_THREE_PASS ? ufc_dev::kParseThreePass
-                                                                             : ufc_dev::kParseFused,
-                       ctx->ncu};
+                       d_items_used};
   if ((e = ufc_dev::parse_batch(a, scratch, need, (hipStream_t)stream)) != hipSuccess) return hip_fail(ctx, e);
   return UFC_OK;
 }
