@@ -112,6 +112,10 @@ __device__ __forceinline__ uint4 fix_piece(const char* lds, uint4 x, int p) {
 }
 
 __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
+#if defined(UFC_TUNING) && defined(UFC_V8_ABL) && (UFC_V8_ABL & 1)  // ablation: no chain steps
+  c.v0 ^= x.x; c.v1 ^= x.y; c.v2 ^= x.z; c.v3 ^= x.w;
+  return;
+#endif
   c.v0 = chain_step(L.lds, c.v0, L.K, x.x);
   c.v1 = chain_step(L.lds, c.v1, L.K, x.y);
   c.v2 = chain_step(L.lds, c.v2, L.K, x.z);
@@ -384,7 +388,11 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   };
   // The result of a set (crc in every lane of a group; trailer word in its lane 7).
   auto finish = [&](uint32_t q, uint32_t geo, const Chains& c, uint32_t voff0, uint64_t sb) {
+#if defined(UFC_TUNING) && defined(UFC_V8_ABL) && (UFC_V8_ABL & 2)  // ablation: no slot combine
+    const uint32_t crc = ~(c.v0 ^ c.v1 ^ c.v2 ^ c.v3 ^ geo);
+#else
     const uint32_t crc = ~unshift(group_lin8(L, c), geo);
+#endif
     const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
     const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     if (SEAL && L.col == 7u && !((geo >> 22) & 1u)) {  // BE32 trailer: one dword store from lane 7
