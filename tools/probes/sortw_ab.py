@@ -47,7 +47,7 @@ for w in WINDOWS:
     else:
         same = torch.equal(ref[0], got[0]) and (SEAL or torch.equal(ref[1], got[1]))
         print(json.dumps({"window": w, "identical_to": WINDOWS[0], "ok": bool(same)}), flush=True)
-        if not same:
+        if not same and os.environ.get("SORTW_NOCHECK") != "1":  # (ablation builds compute garbage)
             sys.exit(1)
 
 times = {w: [] for w in WINDOWS}

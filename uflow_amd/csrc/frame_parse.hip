@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 
 #include "frame_codec_core.hpp"
 #include "frame_parse.hpp"
@@ -139,6 +140,108 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
   if (base != 0xFFFFFFFFu) {  // (each thread reads back only the slots it wrote)
     uint16_t* seg = pos_seg + base;
     for (uint32_t k = 0; k < npos; k++) seg[lo + k] = slots[k * kParseThreads + t];
+  }
+}
+
+// The walk with pooled header slots (round 3): kInlineSlots slots per frame in LDS, and the headers
+// past them in a per-workgroup pool of linked LDS entries (offset | next << 16) taken one at a time
+// with ds_add_rtn.  A frame averages ~15 datagrams, so 16 + a shared pool hold what 64 fixed slots per
+// frame held, in a third of the LDS: more workgroups per CU and more frames walking at once (the walk
+// is a dependent load chain per frame, bound by how many chains are in flight).  A frame that finds
+// the pool full is walked again by the emit step, as one with more than kPosSlots datagrams.
+constexpr uint32_t kInlineSlots = 16;
+constexpr uint32_t kPoolSlots = 2048;
+constexpr uint32_t kPoolNil = 0xFFFFu;
+
+struct PoolSink {
+  static constexpr bool kDecode = false;
+  uint16_t* slot;     // this thread's inline slots (slot k at k * kParseThreads)
+  uint32_t* pool;     // the workgroup's pool
+  uint32_t* ctr;      // its allocation counter
+  uint32_t* head;     // this thread's list (registers, through pointers: the sink is const)
+  uint32_t* tail;
+  bool* full;
+  __device__ bool on() const { return true; }
+  __device__ void operator()(uint32_t, const ufc_item&) const {}
+  __device__ void header(uint32_t k, uint32_t off) const {
+    if (k < kInlineSlots) {
+      slot[k * kParseThreads] = (uint16_t)off;
+      return;
+    }
+    if (*full) return;
+    const uint32_t idx = atomicAdd(ctr, 1u);  // (LDS atomic)
+    if (idx >= kPoolSlots) {
+      *full = true;
+      return;
+    }
+    pool[idx] = off | (kPoolNil << 16);
+    if (k == kInlineSlots)
+      *head = idx;
+    else
+      pool[*tail] = (pool[*tail] & 0xFFFFu) | (idx << 16);
+    *tail = idx;
+  }
+};
+
+__global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const uint8_t* bytes, const uint64_t* offsets,
+                                                                        uint64_t n, const uint8_t* valid,
+                                                                        ufc_frame_info* infos, uint32_t* counts,
+                                                                        uint8_t* modes, uint16_t* pos_seg,
+                                                                        uint32_t* seg_cursor, uint32_t* seg_base,
+                                                                        uint64_t seg_cap) {
+  __shared__ uint16_t slots[kInlineSlots * kParseThreads];
+  __shared__ uint32_t pool[kPoolSlots];
+  __shared__ typename BlockScan::TempStorage scan_tmp;
+  __shared__ uint32_t base_lds, pool_ctr;
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + t;
+  if (t == 0) pool_ctr = 0;
+  __syncthreads();
+  uint32_t npos = 0, head = kPoolNil, tail = kPoolNil;
+  bool full = false;
+  uint8_t mode = kItemsNone;
+  if (i < n) {
+    uint64_t a;
+    const uint32_t len = frame_len32(offsets, i, a);
+    ufc_frame_info info;
+    const bool ok = ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[i] != 0, info,
+                                             PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
+    const uint32_t cnt = ok ? info.item_count : 0u;
+    if (cnt) {
+      if (info.kind == UFC_FRAME_ACK) {
+        mode = kItemsAck;
+      } else if (cnt <= kPosSlots && len <= 0xFFFFu && !full) {
+        mode = kItemsPos;
+        npos = cnt;
+      } else {
+        mode = kItemsWalk;
+      }
+    }
+    info.item_first = 0;  // written by the emit step
+    infos[i] = info;
+    counts[i] = cnt;
+  }
+  uint32_t lo, total;
+  BlockScan(scan_tmp).ExclusiveSum(npos, lo, total);
+  if (t == 0) {
+    uint32_t b = total ? atomicAdd(seg_cursor, total) : 0u;
+    if (total && (uint64_t)b + total > seg_cap) b = 0xFFFFFFFFu;
+    base_lds = b;
+    seg_base[blockIdx.x] = b;
+  }
+  __syncthreads();
+  const uint32_t base = base_lds;
+  if (i < n) modes[i] = (mode == kItemsPos && base == 0xFFFFFFFFu) ? (uint8_t)kItemsWalk : mode;
+  if (base != 0xFFFFFFFFu) {  // (each thread reads back only the slots and list it wrote)
+    uint16_t* seg = pos_seg + base;
+    const uint32_t ni = min(npos, kInlineSlots);
+    for (uint32_t k = 0; k < ni; k++) seg[lo + k] = slots[k * kParseThreads + t];
+    uint32_t idx = head;
+    for (uint32_t k = kInlineSlots; k < npos; k++) {
+      const uint32_t v = pool[idx];
+      seg[lo + k] = (uint16_t)(v & 0xFFFFu);
+      idx = v >> 16;
+    }
   }
 }
 
@@ -290,8 +393,17 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   size_t temp_bytes = lay.end - lay.temp;
   hipError_t e = hipMemsetAsync(cursor, 0, 4, stream);
   if (e != hipSuccess) return e;
-  parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
-                                                                    modes, pos_seg, cursor, bases, lay.seg_cap);
+  bool pool = true;  // pooled header slots (more walking frames per CU); UFC_WALK_POOL=0 (tuning): fixed slots
+#ifdef UFC_TUNING
+  if (const char* w = std::getenv("UFC_WALK_POOL")) pool = std::atoi(w) != 0;
+#endif
+  if (pool)
+    parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
+                                                                           counts, modes, pos_seg, cursor, bases,
+                                                                           lay.seg_cap);
+  else
+    parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
+                                                                      modes, pos_seg, cursor, bases, lay.seg_cap);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
