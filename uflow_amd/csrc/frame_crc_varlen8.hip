@@ -350,7 +350,9 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     const uint32_t J = v8_J(geo), pad = v8_pad(geo);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
     // one select per block (the constant part of each offset goes into the instruction's offset
-    // field; an out-of-range base stays out of range with it)
+    // field; an out-of-range base stays out of range with it).  Every block's load is issued, past
+    // the set's block count too: skipping them under a wave-uniform branch measured 2.29 against
+    // 1.52 ms (the compiler's wait counts no longer match, and it waits for everything).
 #pragma unroll
     for (int j = 0; j < JM; j++) {
       const uint32_t base = ((uint32_t)j < J) ? voff0 : kV8Oob;
