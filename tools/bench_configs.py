@@ -236,8 +236,10 @@ def parse(eng, dev, reps, n=1_000_000):
     med, mean = timed(fn, reps)
     total = int(offsets[-1])
     k = int(used.cpu()[0])
+    # (a checksum of the item records and infos: equal across A/B variants)
+    digest = int(items[:k].view(torch.int64).sum()) ^ int(infos.view(torch.int64).sum())
     return {"config": "f3: device parse (count, scan, fill) of 1M uflow frames after the gate", "frames": n,
-            "frame_bytes": total, "items": k, "ms": round(med, 4), "mean_ms": round(mean, 4),
+            "frame_bytes": total, "items": k, "items_digest": digest, "ms": round(med, 4), "mean_ms": round(mean, 4),
             "frames_per_s": round(n / med * 1e3), "GB_s_of_frame_bytes": round(total / med / 1e-3 / 1e9, 1)}
 
 
