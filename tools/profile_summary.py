@@ -1,6 +1,6 @@
 """profiles/ from a tools/profile_workloads.sh run: copies every workload's kernel-trace stats and
 counter CSVs as profiles/<prefix>_<workload>_{kernel_stats,kernel_trace_dur,pmc_fetch,pmc_write}.*,
-and writes profiles/<prefix>_summary.json: per workload, the kernel(s) it times, the average and
+and writes (merges into) profiles/<prefix>_summary.json: per workload, the kernel(s) it times, the average and
 median dispatch duration from the trace (warm dispatches only), the algorithmic bytes per dispatch,
 the roofline fraction recomputed from them, and FETCH/WRITE bytes per dispatch (FETCH_SIZE KiB x1024
 x2, the gfx950 correction of MI355X_MICROARCH.md; WRITE_SIZE KiB x1024).  Also regenerates
@@ -54,7 +54,9 @@ def main():
     tag, prefix = sys.argv[1], sys.argv[2]
     src = os.path.join(REPO, "gpurun_out", tag)
     dst = os.path.join(REPO, "profiles")
-    summary = {}
+    # (merged into an existing summary: a run over some workloads refreshes only their entries)
+    path = os.path.join(dst, f"{prefix}_summary.json")
+    summary = json.load(open(path)) if os.path.exists(path) else {}
     for w, kernels in WORKLOADS.items():
         kt = os.path.join(src, f"{w}_ktrace")
         if not os.path.isdir(kt):
@@ -82,7 +84,7 @@ def main():
                 algo = line.get("algorithmic_bytes")
             fe = summarise(os.path.join(src, f"{w}_fetch"), sub).get("FETCH_SIZE", {})
             wr = summarise(os.path.join(src, f"{w}_write"), sub).get("WRITE_SIZE", {})
-            ent = {"workload": w, "kernel_substring": sub, "dispatches": len(d),
+            ent = {"workload": w, "run_tag": tag, "kernel_substring": sub, "dispatches": len(d),
                    "avg_us": round(statistics.mean(warm), 2) if warm else None,
                    "median_us": round(statistics.median(warm), 2) if warm else None,
                    "min_us": round(min(warm), 2) if warm else None,
@@ -104,7 +106,7 @@ def main():
     summary["_note"] = ("one process per workload (tools/profile_workloads.sh): <w>_ktrace = rocprofv3 --kernel-trace "
                         "--stats; avg/median over the trace's dispatches of that kernel after the first 5; FETCH/WRITE "
                         "from separate --pmc passes, per dispatch; algorithmic bytes per dispatch as DESIGN.md section 5")
-    with open(os.path.join(dst, f"{prefix}_summary.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(summary, f, indent=1)
     b = summary.get("config 2 validate (bench line)")
     if b and b["fetch_bytes_per_dispatch"] and b["write_bytes_per_dispatch"]:

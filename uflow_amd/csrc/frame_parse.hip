@@ -245,6 +245,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   }
 }
 
+template <int U, bool X4>
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
     const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
@@ -293,48 +294,83 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
   const uint32_t sb = seg_base[blockIdx.x];  // (0xFFFFFFFF: no segment, and no kItemsPos frame either)
   const uint16_t* seg = pos_seg + (sb == 0xFFFFFFFFu ? 0u : sb);
   if (items) {
-    for (uint32_t g = g0 + t; g < g1 && (uint64_t)g < cap; g += kParseThreads) {
-      uint32_t lo_f = 0, hi_f = nb - 1;  // owner: the last frame whose first item is <= g
-      while (lo_f < hi_f) {
-        const uint32_t mid = (lo_f + hi_f + 1) >> 1;
-        if (lfirst[mid] <= g)
-          lo_f = mid;
-        else
-          hi_f = mid - 1;
+    // U items per thread per round (items g, g + 256, ...): every header load of the round is issued
+    // before the first decode and store.  X4: one 16-byte load + one dword per header instead of five
+    // dwords (a straddling dwordx4 is range-checked per dword).
+    const uint64_t g_end = min((uint64_t)g1, cap);
+    for (uint64_t gb = (uint64_t)g0 + t; gb < g_end; gb += (uint64_t)U * kParseThreads) {
+      uint32_t hoff[U], fo[U], x[U][5];
+      uint8_t mm[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint64_t g = gb + (uint64_t)u * kParseThreads;
+        mm[u] = kItemsNone;
+        hoff[u] = fo[u] = 0;
+        if (g < g_end) {
+          uint32_t lo_f = 0, hi_f = nb - 1;  // owner: the last frame whose first item is <= g
+          while (lo_f < hi_f) {
+            const uint32_t mid = (lo_f + hi_f + 1) >> 1;
+            if (lfirst[mid] <= (uint32_t)g)
+              lo_f = mid;
+            else
+              hi_f = mid - 1;
+          }
+          const uint32_t f = lo_f, k = (uint32_t)g - lfirst[f];
+          const uint8_t m = lmode[f];
+          if (m == kItemsPos || m == kItemsAck) {
+            mm[u] = m;
+            fo[u] = f;
+            hoff[u] = m == kItemsPos ? (uint32_t)seg[lseg[f] + k]
+                                     : 1u + ufc_codec::kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
+          }
+        }
       }
-      const uint32_t f = lo_f, k = g - lfirst[f];
-      const uint8_t m = lmode[f];
-      if (m != kItemsPos && m != kItemsAck) continue;
-      const uint32_t hoff = m == kItemsPos ? (uint32_t)seg[lseg[f] + k]
-                                           : 1u + ufc_codec::kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
-      uint32_t w[4];
       if (buf_ok) {
-        const uint32_t rel = (uint32_t)(lstart[f] - span_lo) + delta + hoff;
-        const uint32_t al = rel & ~3u, sh = rel & 3u;
-        uint32_t x[5];
 #pragma unroll
-        for (int q = 0; q < 5; q++) x[q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(al + 4 * q), 0, 0);
+        for (int u = 0; u < U; u++) {
+          if (mm[u] == kItemsNone) continue;
+          const uint32_t al = ((uint32_t)(lstart[fo[u]] - span_lo) + delta + hoff[u]) & ~3u;
+          if constexpr (X4) {
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)al, 0, 0);
+            x[u][0] = v.x, x[u][1] = v.y, x[u][2] = v.z, x[u][3] = v.w;
+            x[u][4] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(al + 16), 0, 0);
+          } else {
 #pragma unroll
-        for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbyte(x[q + 1], x[q], sh);
-      } else {
-        const DevBytes rd{bytes + lstart[f] + hoff};
-#pragma unroll
-        for (int q = 0; q < 4; q++) w[q] = 0;
-        // (only the bytes the header occupies: a datagram's hs <= 14, an ack group 9)
-        const uint32_t nbytes = m == kItemsAck ? UFC_ACK_GROUP_SIZE : 14u;
-        for (uint32_t c = 0; c < nbytes; c++) w[c >> 2] |= rd(c) << (8 * (c & 3));
+            for (int q = 0; q < 5; q++) x[u][q] = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(al + 4 * q), 0, 0);
+          }
+        }
       }
-      auto h = [&](uint32_t c) -> uint32_t { return (w[c >> 2] >> (8 * (c & 3))) & 0xFFu; };
-      ufc_item it{};
-      if (m == kItemsPos) {
-        uint32_t hs, dl;
-        ufc_codec::datagram_size(h, hs, dl);
-        ufc_codec::decode_datagram(h, hs, it);
-        it.data_offset = hoff + hs;
-      } else {
-        ufc_codec::decode_ack_group(h, it);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint8_t m = mm[u];
+        if (m == kItemsNone) continue;
+        const uint32_t f = fo[u];
+        uint32_t w[4];
+        if (buf_ok) {
+          const uint32_t sh = ((uint32_t)(lstart[f] - span_lo) + delta + hoff[u]) & 3u;
+#pragma unroll
+          for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbyte(x[u][q + 1], x[u][q], sh);
+        } else {
+          const DevBytes rd{bytes + lstart[f] + hoff[u]};
+#pragma unroll
+          for (int q = 0; q < 4; q++) w[q] = 0;
+          // (only the bytes the header occupies: a datagram's hs <= 14, an ack group 9)
+          const uint32_t nbytes = m == kItemsAck ? UFC_ACK_GROUP_SIZE : 14u;
+          for (uint32_t c = 0; c < nbytes; c++) w[c >> 2] |= rd(c) << (8 * (c & 3));
+        }
+        auto h = [&](uint32_t c) -> uint32_t { return (w[c >> 2] >> (8 * (c & 3))) & 0xFFu; };
+        ufc_item it{};
+        if (m == kItemsPos) {
+          uint32_t hs, dl;
+          ufc_codec::datagram_size(h, hs, dl);
+          ufc_codec::decode_datagram(h, hs, it);
+          it.data_offset = hoff[u] + hs;
+        } else {
+          ufc_codec::decode_ack_group(h, it);
+        }
+        store_item(items + gb + (uint64_t)u * kParseThreads, it);
       }
-      store_item(items + g, it);
     }
     // Frames whose headers did not fit the slots: walked again, items stored directly.
     if (mode == kItemsWalk && (uint64_t)first < cap) {
@@ -408,7 +444,21 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
   if (e != hipSuccess) return e;
-  parse_emit_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
+  // One item per thread per round, 16-byte header loads (0.526 against 0.551 ms with five dword loads;
+  // 4 items per round 0.532 with them, 0.543 without: DESIGN.md section 5.5).
+  auto emit = parse_emit_kernel<1, true>;
+#ifdef UFC_TUNING
+  {  // UFC_EMIT_U=1|2|4 items per thread per round, UFC_EMIT_X4=0: five dword loads per header
+    const char* wu = std::getenv("UFC_EMIT_U");
+    const char* wx = std::getenv("UFC_EMIT_X4");
+    const int eu = wu ? std::atoi(wu) : 1;
+    const bool x4 = !wx || std::atoi(wx) != 0;
+    if (eu == 2) emit = x4 ? parse_emit_kernel<2, true> : parse_emit_kernel<2, false>;
+    else if (eu == 4) emit = x4 ? parse_emit_kernel<4, true> : parse_emit_kernel<4, false>;
+    else if (!x4) emit = parse_emit_kernel<1, false>;
+  }
+#endif
+  emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
                                                                     firsts, modes, pos_seg, bases, a.items, a.items_cap,
                                                                     a.items_used);
   return hipGetLastError();
