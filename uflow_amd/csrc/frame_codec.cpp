@@ -15,6 +15,7 @@ namespace {
 struct HostBytes {
   const uint8_t* p;
   uint32_t operator()(uint32_t i) const { return p[i]; }
+  uint32_t head3(uint32_t i) const { return p[i] | (p[i + 1] << 8) | ((uint32_t)p[i + 2] << 16); }
 };
 
 inline void put32(uint8_t* p, uint32_t v) {

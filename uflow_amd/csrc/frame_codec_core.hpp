@@ -4,7 +4,8 @@
 // Restates src/frame/serial/mod.rs:694-705 (dispatch on the frame id) and read_*_payload :54-434,
 // read_datagram :183-309.  A byte reader abstracts the frame: rd(i) = frame byte i (i < len).
 // Only bytes the reference reads are read, in the order it checks lengths, so a rejected frame
-// never reads past its end.
+// never reads past its end.  rd.head3(i) = bytes i, i + 1, i + 2 packed little-endian (the caller has
+// checked that at least 6 bytes remain from i; a reader may read byte i + 3 with them).
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -159,8 +160,11 @@ UFC_HD bool parse_payload(const Rd& rd, uint32_t len, ufc_frame_info& info, cons
         const uint32_t rem = plen - pos;
         if (rem < 6) return false;
         auto h = [&](uint32_t c) -> uint32_t { return p(pos + c); };
+        // the header's first three bytes at once (rd.head3: one read where the reader can, so the
+        // sizes of small and large datagrams do not wait on a second read after the first byte's)
+        const uint32_t h3 = rd.head3(1 + pos);
         uint32_t hs, dl;
-        datagram_size(h, hs, dl);
+        datagram_size([&](uint32_t c) -> uint32_t { return (h3 >> (8 * c)) & 0xFFu; }, hs, dl);
         if (rem < hs + dl) return false;
         if (items.on() && k < cap) {
           if (Sink::kDecode) {

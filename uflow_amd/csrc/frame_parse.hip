@@ -48,6 +48,11 @@ struct DevBytes {
   __device__ uint32_t operator()(uint32_t i) const {
     return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
   }
+  // one dword load at any byte address (gfx950's unaligned access mode; the codec guarantees the
+  // four bytes lie inside the frame): one round trip and one address pass for a datagram's sizes
+  __device__ uint32_t head3(uint32_t i) const {
+    return *(const __attribute__((address_space(1))) uint32_t*)(p + i) & 0xFFFFFFu;
+  }
 };
 
 // Walk sink: only the header offsets, into this thread's LDS slots (slot k at k * kParseThreads).
