@@ -55,6 +55,24 @@ struct DevBytes {
   }
 };
 
+// The walk's reader: the frame's first 8 bytes (kind, the data header's fields) come from one 8-byte
+// load issued with the frame's other first reads when the frame has 8 bytes; the rest as DevBytes.
+struct DevBytesHead {
+  const uint8_t* p;
+  uint64_t w;  // bytes 0..7, little-endian
+  bool has8;
+  __device__ static uint64_t load8(const uint8_t* q) {  // (any byte address: unaligned access mode)
+    return *(const __attribute__((address_space(1))) uint64_t*)q;
+  }
+  __device__ uint32_t operator()(uint32_t i) const {
+    if (has8 && i < 8) return (uint32_t)(w >> (8 * i)) & 0xFFu;
+    return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
+  }
+  __device__ uint32_t head3(uint32_t i) const {
+    return *(const __attribute__((address_space(1))) uint32_t*)(p + i) & 0xFFFFFFu;
+  }
+};
+
 // Walk sink: only the header offsets, into this thread's LDS slots (slot k at k * kParseThreads).
 struct PosSink {
   static constexpr bool kDecode = false;
@@ -209,7 +227,9 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
-    const bool ok = ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[i] != 0, info,
+    const bool has8 = len >= 8;
+    const DevBytesHead rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8};
+    const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
     const uint32_t cnt = ok ? info.item_count : 0u;
     if (cnt) {
