@@ -48,17 +48,11 @@ def _stamp_ok(target, digest):
         return False
 
 
-def build_native(force=False, verbose=False, tuning=False, out=None, defines=()):
-    """tuning=True adds the ablation kernels (-DUFC_TUNING); `defines` adds -D flags (tuning
-    experiments).  Both are meant with `out` pointing away from the product library.
-
-    Rebuilds when the sha256 of the sources, headers, flags and this file differs from the one
-    recorded beside the library (<lib>.sha256), not by file times: a library copied to another
-    machine (the GPU box) with its stamp is rebuilt there only if it does not match the source."""
+def _native_identity(tuning=False, defines=()):
+    """(sources, hipcc flags, digest) of a native build from the sources in this tree."""
     sources = SOURCES + (TUNING_SOURCES if tuning else [])
     deps = [os.path.join(CSRC, s) for s in sources + HEADERS]
     deps += [os.path.join(REPO_DIR, "include", h) for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
-    target = out or LIB_PATH
     # No atomic optimizer: the lean kernel's single-lane claim atomics must stay plain
     # global_atomic_add (the optimizer reads the result back at once, forcing a vmcnt(0) wait).
     flags = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall",
@@ -66,7 +60,23 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
     if tuning:
         flags.append("-DUFC_TUNING")
     flags += ["-D" + d for d in defines]
-    digest = _digest(deps + [os.path.abspath(__file__)], flags[1:])
+    return sources, flags, _digest(deps + [os.path.abspath(__file__)], flags[1:])
+
+
+def tuning_lib_current(path):
+    """Whether the tuning library at `path` was built from this tree's sources (its stamp)."""
+    return _stamp_ok(path, _native_identity(tuning=True)[2])
+
+
+def build_native(force=False, verbose=False, tuning=False, out=None, defines=()):
+    """tuning=True adds the ablation kernels (-DUFC_TUNING); `defines` adds -D flags (tuning
+    experiments).  Both are meant with `out` pointing away from the product library.
+
+    Rebuilds when the sha256 of the sources, headers, flags and this file differs from the one
+    recorded beside the library (<lib>.sha256), not by file times: a library copied to another
+    machine (the GPU box) with its stamp is rebuilt there only if it does not match the source."""
+    sources, flags, digest = _native_identity(tuning, defines)
+    target = out or LIB_PATH
     if not force and _stamp_ok(target, digest):
         return target
     # One object per source, compiled in parallel, then one link (every object: the stamp differs).

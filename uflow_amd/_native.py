@@ -12,6 +12,11 @@ from ._build import LIB_PATH as _DEFAULT_LIB
 
 # UFC_LIB overrides the library path (tuning builds only; the product loads the in-tree .so).
 LIB_PATH = os.environ.get("UFC_LIB", _DEFAULT_LIB)
+if os.path.basename(LIB_PATH).startswith("libuflowcrc_tuning") and os.environ.get("UFC_LIB_ANY") != "1":
+    from ._build import tuning_lib_current as _current
+    if not _current(LIB_PATH):  # (an A/B against a stale tuning build measures old code)
+        raise RuntimeError(f"{LIB_PATH} was not built from this tree's sources: rebuild it with "
+                           "build_native(tuning=True, out=...) (or set UFC_LIB_ANY=1)")
 
 UFC_OK = 0
 UFC_ERR_INVALID_ARG = -1
