@@ -129,11 +129,64 @@ def affinity_cpus():
         return os.cpu_count() or 1
 
 
+def cgroup_cpu_quota():
+    """The CPU bandwidth quota of this process's cgroup in CPUs (quota / period), or None if unlimited
+    or unreadable: cgroup v2 cpu.max, else v1 cpu.cfs_quota_us / cpu.cfs_period_us."""
+    rel = ""
+    try:
+        with open("/proc/self/cgroup") as f:
+            for line in f:
+                parts = line.strip().split(":", 2)
+                if len(parts) == 3 and (parts[0] == "0" or "cpu" in parts[1].split(",")):
+                    rel = parts[2]
+                    if parts[0] == "0":
+                        break
+    except OSError:
+        pass
+    cands = []
+    for d in ([os.path.join("/sys/fs/cgroup", rel.lstrip("/"))] if rel else []) + ["/sys/fs/cgroup"]:
+        cands.append(("v2", os.path.join(d, "cpu.max"), None))
+    for d in ([os.path.join("/sys/fs/cgroup/cpu", rel.lstrip("/"))] if rel else []) + ["/sys/fs/cgroup/cpu",
+                                                                                       "/sys/fs/cgroup/cpu,cpuacct"]:
+        cands.append(("v1", os.path.join(d, "cpu.cfs_quota_us"), os.path.join(d, "cpu.cfs_period_us")))
+    for kind, qpath, ppath in cands:
+        try:
+            if kind == "v2":
+                with open(qpath) as f:
+                    q, p = f.read().split()[:2]
+                if q == "max":
+                    return None, qpath
+                return int(q) / int(p), qpath
+            with open(qpath) as f:
+                q = int(f.read().strip())
+            with open(ppath) as f:
+                p = int(f.read().strip())
+            return (None if q <= 0 else q / p), qpath
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
+def effective_cpus():
+    """(threads to use, how they were chosen): the cgroup CPU quota if there is one, else the box's
+    declared CPU share (OMP_NUM_THREADS, set to the per-GPU share on the GPU box), never more than the
+    affinity mask."""
+    aff = affinity_cpus()
+    quota, qsrc = cgroup_cpu_quota()
+    if quota is not None:
+        return max(1, min(aff, int(quota))), f"cgroup quota {quota:g} CPUs ({qsrc})"
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        return min(aff, int(omp)), f"no cgroup quota; OMP_NUM_THREADS={omp} (the box's CPU share)"
+    return aff, "no cgroup quota, no OMP_NUM_THREADS; affinity mask"
+
+
 def cpu_baseline(host, n, L, target_s):
     """The oracle -- a C restatement of the reference's own loop, crc.rs:94-100 (one table load per
-    byte) behind the gate of serial/mod.rs:675-690 -- on the host cores: one thread, then every CPU
-    this process may run on, frames split contiguously; each leg on a bounded sample of config 2's
-    frames, repeated for about target_s seconds."""
+    byte) behind the gate of serial/mod.rs:675-690 -- on the host cores: one thread, then as many
+    threads as the process's effective CPU share (cgroup quota, else the box's declared share, never
+    more than the affinity mask), frames split contiguously; each leg on a bounded sample of config
+    2's frames, repeated for about target_s seconds."""
     import oracle
 
     def leg(threads, sample):
@@ -148,19 +201,35 @@ def cpu_baseline(host, n, L, target_s):
         dt = time.perf_counter() - t0
         return sample * L * reps / dt / 2**30, reps
 
-    threads = affinity_cpus()
+    threads, how = effective_cpus()
+    quota, _ = cgroup_cpu_quota()
     s1 = min(n, 20_000)
     v1, r1 = leg(1, s1)
     sn = min(n, max(s1, 20_000 * threads))
     vn, rn = leg(threads, sn)
     return {
         "value": round(vn, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-        "single_core_value": round(v1, 4), "nproc": os.cpu_count(), "affinity_cpus": threads,
+        "single_core_value": round(v1, 4), "nproc": os.cpu_count(), "affinity_cpus": affinity_cpus(),
+        "effective_cpus": threads, "cgroup_quota_cpus": quota, "cores_source": how,
         "sample": f"config 2 frames (first of the batch): {s1} x {L} B x {r1} reps on 1 thread, {sn} x {L} B x "
-                  f"{rn} reps on {threads} threads (all CPUs in this process's affinity; os.cpu_count() = "
+                  f"{rn} reps on {threads} threads ({how}; affinity {affinity_cpus()} CPUs, os.cpu_count() = "
                   f"{os.cpu_count()}); bytewise table loop of crc.rs:94-100 in C (oracle/crc_oracle.c), "
                   f"frames split contiguously over the threads",
     }
+
+
+def shard_reference(frames, n, L, threads, chunk=1 << 20):
+    """The oracle's CRC words and valid flags of n fixed frames held on the device (uint8[n * L]),
+    copied back and checked chunk by chunk."""
+    import oracle
+    ref_crc = np.empty(n, np.uint32)
+    ref_valid = np.empty(n, np.uint8)
+    for c0 in range(0, n, chunk):
+        m = min(chunk, n - c0)
+        c, v = oracle.validate_fixed_mt(frames[c0 * L:(c0 + m) * L].cpu().numpy(), L, L, m, threads)
+        ref_crc[c0:c0 + m] = c
+        ref_valid[c0:c0 + m] = v
+    return ref_crc, ref_valid
 
 
 def launch_ranks(a):
@@ -357,34 +426,50 @@ def main():
         ceiling = read_ceiling(eng, frames[: min(n, 1 << 22) * L], compute)
 
     # ---- correctness (after the timed region) ----
-    import oracle
     crc, valid = slots[last]
     ok, parity = True, ""
-    if rank == 0:
+    if not sharded:
+        import oracle
         h_valid = valid.cpu().numpy()
         ok = bool(np.array_equal(h_valid, expected_valid(0, total, a.flip_every)))
         h_crc = crc.cpu().numpy().view(np.uint32)
-        if not sharded:
-            host = frames.cpu().numpy()
-            ref_crc, ref_valid = oracle.validate_fixed_mt(host, L, L, n, min(64, affinity_cpus()))
-            exact = bool(np.array_equal(h_crc, ref_crc) and np.array_equal(h_valid, ref_valid))
-            parity = f"every frame bit-exact vs the CPU oracle: {exact}"
-        else:
-            # a sample of every rank's shard, regenerated here: the CRC word is compute(frame[..-4]),
-            # independent of the trailer, so the oracle needs only the (flipped) synthetic bytes
-            exact = True
+        host = frames.cpu().numpy()
+        ref_crc, ref_valid = oracle.validate_fixed_mt(host, L, L, n, effective_cpus()[0])
+        exact = bool(np.array_equal(h_crc, ref_crc) and np.array_equal(h_valid, ref_valid))
+        parity = f"every frame bit-exact vs the CPU oracle: {exact}"
+        ok = ok and exact
+    else:
+        # Every CRC word that reached the root: each rank runs the oracle over its own shard's frames
+        # (the bytes the gate read, copied back in chunks) and sends the words to the root, which
+        # compares them with the gathered words at their global positions; every valid flag is
+        # compared with the planted flips.
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        threads = max(1, effective_cpus()[0] // max(1, local_world))
+        t_chk = time.perf_counter()
+        ref_crc, ref_valid = shard_reference(frames, n, L, threads)
+        local_ok = bool(np.array_equal(ref_valid, expected_valid(lo, n, a.flip_every)))
+        exact = True
+        if rank == 0:
+            g_valid = valid.cpu().numpy()
+            ok = bool(np.array_equal(g_valid, expected_valid(0, total, a.flip_every)))
             for r in range(world):
                 rlo, rhi = shard_of(total, r, world)
-                for s0 in (rlo, (rlo + rhi) // 2, max(rlo, rhi - 2000)):
-                    m = min(2000, rhi - s0)
-                    sample = synth.fixed_frames(m, L, seed, first_frame=s0, device=dev)
-                    fl = np.nonzero(expected_valid(s0, m, a.flip_every) == 0)[0]
-                    if fl.size:
-                        synth.flip_bits(sample, torch.from_numpy(fl * L).to(dev))
-                    ref_crc, _ = oracle.validate_fixed(sample.cpu().numpy(), L, L, m)
-                    exact = exact and bool(np.array_equal(h_crc[s0:s0 + m], ref_crc))
-            parity = f"valid flags of all {total} frames + 3 x 2000 CRC words per rank bit-exact vs the oracle: {exact}"
-        ok = ok and exact
+                if r == 0:
+                    ref_r = torch.from_numpy(ref_crc.view(np.int32)).to(dev)
+                else:
+                    ref_r = torch.empty(rhi - rlo, dtype=torch.int32, device=dev)
+                    if rhi > rlo:
+                        dist.recv(ref_r, src=r)
+                exact = exact and bool(torch.equal(crc[rlo:rhi], ref_r))
+        elif n > 0:
+            dist.send(torch.from_numpy(ref_crc.view(np.int32)).to(dev), dst=0)
+        flag = torch.tensor([0 if local_ok else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        all_local_ok = int(flag.item()) == 0
+        parity = (f"all {total} CRC words gathered on rank 0 == the CPU oracle over every rank's shard: {exact}; "
+                  f"oracle valid flags == planted flips on every rank: {all_local_ok} "
+                  f"({time.perf_counter() - t_chk:.1f} s, {threads} threads per rank)")
+        ok = ok and exact and all_local_ok
 
     result = None
     if rank == 0:

@@ -57,6 +57,8 @@ extern "C" {
 #define UFC_ERR_HIP (-3)
 #define UFC_ERR_NOMEM (-4)
 #define UFC_ERR_COMM (-5) /* RCCL missing or failed (multi-GPU entry points; see ufc_comm_last_error) */
+#define UFC_ERR_PEER (-6) /* multi-GPU: another rank rejected its part of this call; nothing was transferred */
+#define UFC_ERR_TIMEOUT (-7) /* multi-GPU: the peers did not join the call's status agreement in time */
 
 /* Frame constants from the reference (src/frame/serial/mod.rs:11-13, src/lib.rs:286-294). */
 #define UFC_FRAME_CRC_SIZE 4
@@ -216,6 +218,9 @@ int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const ui
 int ufc_comm_destroy(ufc_comm* comm);
 /* Last RCCL result code seen by this communicator (0 if none). */
 int ufc_comm_last_error(const ufc_comm* comm);
+/* How long a sharded call waits for the peers to join its status agreement (below) before it aborts
+ * the communicator and returns UFC_ERR_TIMEOUT; 0 = forever.  Default 300000 ms. */
+int ufc_comm_set_timeout(ufc_comm* comm, int timeout_ms);
 /* Collective: the batched gate on this rank's shard, then the gather to `root`.
  *   d_frames     this rank's shard (frame k of the shard at d_frames + k * stride, stride >= frame_len)
  *   d_crc_out    root: n_total words in global frame order; other ranks: their shard's words
@@ -227,10 +232,15 @@ int ufc_comm_last_error(const ufc_comm* comm);
  *                once gather_stream has passed this call.
  * One host thread per communicator at a time; every rank must make the same calls in the same
  * order with the same n_total, stride, frame_len, root and output nullness.  Arguments that every
- * rank sees alike are checked before any transfer, so a bad call fails on every rank.  A failure
- * that only this rank sees after the gather has begun (a HIP launch error) aborts the communicator
- * (ncclCommAbort) and marks it unusable (later calls return UFC_ERR_COMM): the peers' transfers
- * then fail or stall, and the caller must tear down every rank's communicator. */
+ * rank sees alike are checked before any transfer, so a bad call fails on every rank.  Arguments
+ * only this rank can check (its shard pointers) are agreed before any transfer with a one-word
+ * all-reduce on a second communicator: a rank that rejects its part returns UFC_ERR_INVALID_ARG,
+ * every other rank UFC_ERR_PEER, nothing is queued and the communicator stays usable.  That wait has
+ * a deadline (ufc_comm_set_timeout): a peer that never joins aborts the communicator
+ * (UFC_ERR_TIMEOUT).  A failure that only this rank sees after the gather has begun (a HIP launch
+ * error) aborts the communicator (ncclCommAbort) and marks it unusable (later calls return
+ * UFC_ERR_COMM): the peers' transfers then fail or stall, and the caller must tear down every
+ * rank's communicator. */
 int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size_t frame_len, uint64_t n_total,
                     uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream);
 /* Variable-length form: rank r's shard is the frames [bounds[r], bounds[r+1]) (ufc_shard_bounds_varlen

@@ -6,6 +6,12 @@ its socket transport over loopback: the N > 1 branch of ufc_crc_sharded / ufc_cr
 the ncclSend of every sender, the root's ncclRecv into global frame order, the chunk pipeline on a
 separate gather stream -- runs for real, only over a slower wire than xGMI.  The root checks every
 gathered CRC word and valid flag against the CPU oracle over the whole batch and prints one JSON line (the fixed batch's root is the last rank, the variable-length batch's rank 0).
+Then a rank-local failure: the last rank passes no shard (NULL frames); every rank must return an
+error (that rank UFC_ERR_INVALID_ARG, the others UFC_ERR_PEER) instead of hanging, and the next call
+on the same communicator must succeed.
+--timeout (world 2): rank 0 calls alone with a 3 s deadline and must get UFC_ERR_TIMEOUT; rank 1
+calls only afterwards and must fail too (timeout or the aborted peer); both then destroy their
+aborted communicators.
 """
 import json
 import os
@@ -91,6 +97,32 @@ def main():
         result["varlen_invalid"] = int(total - ref_valid.sum())
         result["varlen_bounds"] = [int(x) for x in b]
 
+    # ---- a rank-local failure, agreed before any transfer ----
+    from uflow_amd._native import NativeError
+    total, L, root = 100_000, 64, 0
+    b = shard_bounds_fixed(total, world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    frames = fixed_batch(lo, hi - lo)
+    n_out = total if rank == root else hi - lo
+    crc = torch.full((n_out,), -1, dtype=torch.int32, device=dev)
+    bad = rank == world - 1
+    try:
+        gate.crc_sharded(None if bad else frames, L, total, crc, None, root=root, gather_stream=gs)
+        code = 0
+    except NativeError as e:
+        code = e.code
+    torch.cuda.synchronize()
+    codes = torch.zeros(world, dtype=torch.int32, device=dev)
+    codes[rank] = code
+    dist.all_reduce(codes)
+    gate.crc_sharded(frames, L, total, crc, None, root=root, gather_stream=gs)  # the comm still works
+    torch.cuda.synchronize()
+    if rank == root:
+        host = fixed_batch(0, total).cpu().numpy()
+        ref_crc, _ = oracle.validate_fixed_mt(host, L, L, total, 16)
+        result["fail_codes"] = [int(x) for x in codes.cpu()]
+        result["after_fail_crc_ok"] = bool(np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc))
+
     gate.close()
     dist.barrier()
     dist.destroy_process_group()
@@ -99,5 +131,47 @@ def main():
         print(json.dumps(result), flush=True)
 
 
+def timeout_main():
+    """World 2: rank 0 calls alone and must time out; rank 1 calls late and must fail as well."""
+    from uflow_amd._native import NativeError
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    eng = FrameCrcEngine(0)
+    idt = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        idt.copy_(torch.frombuffer(bytearray(comm_id_create()), dtype=torch.uint8))
+    dist.broadcast(idt, src=0)
+    gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
+    gate.set_timeout(3000)
+    total, L = 1000, 64
+    b = shard_bounds_fixed(total, world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    frames = synth.fixed_frames(hi - lo, L, synth.SEED_CONFIG4, first_frame=lo, device=dev)
+    crc = torch.zeros(total if rank == 0 else hi - lo, dtype=torch.int32, device=dev)
+    import time
+    code = 0
+    if rank != 0:
+        dist.barrier()  # after rank 0 has timed out
+    t0 = time.monotonic()
+    try:
+        gate.crc_sharded(frames, L, total, crc, None, root=0)
+    except NativeError as e:
+        code = e.code
+    waited = time.monotonic() - t0
+    if rank == 0:
+        dist.barrier()
+    gate.close()  # destroy after abort
+    codes = torch.zeros(world, dtype=torch.int32, device=dev)
+    codes[rank] = code
+    dist.all_reduce(codes)
+    if rank == 0:
+        print(json.dumps({"timeout_codes": [int(x) for x in codes.cpu()], "rank0_waited_s": round(waited, 2)}),
+              flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    eng.close()
+
+
 if __name__ == "__main__":
-    main()
+    timeout_main() if "--timeout" in sys.argv else main()

@@ -86,11 +86,7 @@ def test_sharded_varlen_world1_config3(engine, gate):
     assert int(ref_valid.sum()) == n - len(range(0, n, 1001))
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ranks_on_one_device(world):
-    """The N > 1 send/recv branch of the C ABI, executed: `world` ranks on cuda:0, RCCL over its
-    socket transport (each rank on its own NCCL_HOSTID), fixed and variable-length batches gathered
-    to a root and checked frame by frame against the oracle (tests/gpu_shard_worker.py)."""
+def _run_worker(world, args, timeout):
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -99,8 +95,16 @@ def test_ranks_on_one_device(world):
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(repo, "tests", "gpu_shard_worker.py")]
-    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=repo)
+           os.path.join(repo, "tests", "gpu_shard_worker.py")] + args
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=repo)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_on_one_device(world):
+    """The N > 1 send/recv branch of the C ABI, executed: `world` ranks on cuda:0, RCCL over its
+    socket transport (each rank on its own NCCL_HOSTID), fixed and variable-length batches gathered
+    to a root and checked frame by frame against the oracle (tests/gpu_shard_worker.py)."""
+    p = _run_worker(world, [], 240)
     assert p.returncode == 0, p.stderr[-3000:]
     # one JSON object per root (last rank: fixed; rank 0: varlen); the two processes share the pipe,
     # so their lines may arrive on one line
@@ -113,3 +117,19 @@ def test_ranks_on_one_device(world):
     assert j["fixed_crc_ok"] and j["fixed_valid_ok"] and j["fixed_invalid"] == len(range(0, 9_000_001, 1013))
     assert j["varlen_crc_ok"] and j["varlen_valid_ok"] and j["varlen_invalid"] == len(range(0, 1_500_001, 7))
     assert len(j["varlen_bounds"]) == world + 1 and 0 < j["varlen_bounds"][1] < 1_500_001
+    # the last rank passed no shard: it gets UFC_ERR_INVALID_ARG (-1), every other rank UFC_ERR_PEER
+    # (-6), nobody hangs, and the next call on the same communicators is exact
+    assert j["fail_codes"] == [-6] * (world - 1) + [-1]
+    assert j["after_fail_crc_ok"]
+
+
+def test_sharded_peer_timeout():
+    """ufc_comm_set_timeout: rank 0 of 2 calls alone and gets UFC_ERR_TIMEOUT (-7) after its 3 s
+    deadline (communicator aborted); rank 1 calls afterwards and fails too; both destroy their
+    aborted communicators (tests/gpu_shard_worker.py --timeout)."""
+    p = _run_worker(2, ["--timeout"], 180)
+    assert p.returncode == 0, p.stderr[-3000:]
+    j = json.loads(re.findall(r"\{[^{}]*\}", p.stdout)[0])
+    assert j["timeout_codes"][0] == -7, j
+    assert j["timeout_codes"][1] in (-7, -5), j
+    assert 2.5 < j["rank0_waited_s"] < 30, j

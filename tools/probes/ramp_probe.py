@@ -52,7 +52,8 @@ for r in range(5):
     for n in sizes:
         res["gate"][n].append(timed(gate, n))
         res["stream"][n].append(timed(stream, n))
-ok = int(valid.sum()) == NMAX  # (seal_fixed above re-sealed every frame)
+nvalid = int(valid.sum())  # the last launch gated all NMAX frames of the GPU-sealed batch
+ok = nvalid == NMAX
 for k, d in res.items():
     x = np.array([n * L for n in sizes], dtype=np.float64)
     y = np.array([float(np.median(d[n])) for n in sizes])
@@ -60,4 +61,6 @@ for k, d in res.items():
     print(json.dumps({"kernel": k, "ms_median": {str(n): round(float(np.median(d[n])), 4) for n in sizes},
                       "marginal_TBs": round(1e-9 / slope, 3), "fixed_us_per_launch": round(icpt * 1e3, 2),
                       "frac_at_1M": round(1.505e9 / (float(np.median(d[1_000_000])) * 1e-3) / 8e12, 4),
-                      "valid_counts_ok": ok}), flush=True)
+                      "valid_count": nvalid, "valid_counts_ok": ok}), flush=True)
+if not ok:
+    sys.exit(f"self-check failed: {nvalid} of {NMAX} sealed frames valid")

@@ -509,6 +509,8 @@ const char* ufc_error_string(int code) {
     case UFC_ERR_HIP: return "HIP runtime error (see ufc_ctx_last_hip_error)";
     case UFC_ERR_NOMEM: return "out of memory";
     case UFC_ERR_COMM: return "RCCL unavailable or failed (see ufc_comm_last_error)";
+    case UFC_ERR_PEER: return "another rank rejected its part of this sharded call (nothing was transferred)";
+    case UFC_ERR_TIMEOUT: return "the peer ranks did not join the sharded call in time (communicator aborted)";
     default: return "unknown error";
   }
 }

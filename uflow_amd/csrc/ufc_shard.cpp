@@ -16,10 +16,12 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 
 #include "../../include/uflow_frame_crc.h"
 #include "ufc_internal.hpp"
@@ -33,6 +35,9 @@ struct Rccl {
   ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
   ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
   ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
+  ncclResult_t (*CommSplit)(ncclComm_t, int, int, ncclComm_t*, ncclConfig_t*) = nullptr;
+  ncclResult_t (*CommGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*AllReduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*Recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
   ncclResult_t (*GroupStart)() = nullptr;
@@ -56,12 +61,15 @@ const Rccl& rccl() {
     r.CommInitRank = (decltype(r.CommInitRank))sym("ncclCommInitRank");
     r.CommDestroy = (decltype(r.CommDestroy))sym("ncclCommDestroy");
     r.CommAbort = (decltype(r.CommAbort))sym("ncclCommAbort");
+    r.CommSplit = (decltype(r.CommSplit))sym("ncclCommSplit");
+    r.CommGetAsyncError = (decltype(r.CommGetAsyncError))sym("ncclCommGetAsyncError");
+    r.AllReduce = (decltype(r.AllReduce))sym("ncclAllReduce");
     r.Send = (decltype(r.Send))sym("ncclSend");
     r.Recv = (decltype(r.Recv))sym("ncclRecv");
     r.GroupStart = (decltype(r.GroupStart))sym("ncclGroupStart");
     r.GroupEnd = (decltype(r.GroupEnd))sym("ncclGroupEnd");
-    r.ok = r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.CommAbort && r.Send && r.Recv && r.GroupStart &&
-           r.GroupEnd;
+    r.ok = r.GetUniqueId && r.CommInitRank && r.CommDestroy && r.CommAbort && r.CommSplit && r.CommGetAsyncError &&
+           r.AllReduce && r.Send && r.Recv && r.GroupStart && r.GroupEnd;
   });
   return r;
 }
@@ -90,6 +98,14 @@ struct ufc_comm {
   int nranks = 0;
   int rank = 0;
   ncclComm_t nccl = nullptr;
+  // Status agreement before every gather (agree_status): a second communicator split from the first,
+  // so that its one-word all-reduce never queues behind the data communicator's transfers, on a
+  // stream of its own; the word goes through pinned host memory.
+  ncclComm_t ctl = nullptr;
+  hipStream_t ctl_stream = nullptr;
+  int32_t* d_status = nullptr;
+  int32_t* h_status = nullptr;  // [0] this rank's status, [1] the agreed (max over ranks)
+  int timeout_ms = 300000;
   int last_nccl_error = 0;
   bool broken = false;  // aborted after a rank-local failure mid-gather: every later call fails
   hipEvent_t ev[kMaxChunks] = {};
@@ -157,9 +173,54 @@ int nccl_fail(ufc_comm* comm, ncclResult_t r) {
 // later call queues transfers the peers cannot match.
 int abort_comm(ufc_comm* comm, int rc) {
   if (comm->nccl && !comm->broken) (void)rccl().CommAbort(comm->nccl);
+  if (comm->ctl && !comm->broken) (void)rccl().CommAbort(comm->ctl);
   comm->nccl = nullptr;
+  comm->ctl = nullptr;
   comm->broken = true;
   return rc;
+}
+
+// Every rank's verdict on its own arguments, agreed before any transfer is queued: a one-word
+// max-all-reduce on the control communicator, read back through pinned memory.  A rank-local failure
+// (a missing shard pointer) then fails the call on every rank -- UFC_ERR_PEER on the others -- and
+// the communicator stays usable.  The wait polls with a deadline (timeout_ms): a peer that never
+// makes the call (crashed, or calling something else) aborts both communicators instead of hanging.
+int agree_status(ufc_comm* comm, int local_rc) {
+  if (comm->nranks == 1) return local_rc;
+  const Rccl& r = rccl();
+  comm->h_status[0] = local_rc != UFC_OK ? 1 : 0;
+  comm->h_status[1] = -1;
+  hipError_t e = hipMemcpyAsync(comm->d_status, comm->h_status, 4, hipMemcpyHostToDevice, comm->ctl_stream);
+  if (e != hipSuccess) {
+    ufc_internal::note_hip_error(comm->ctx, (int)e);
+    return abort_comm(comm, UFC_ERR_HIP);
+  }
+  const ncclResult_t nr = r.AllReduce(comm->d_status, comm->d_status, 1, ncclInt32, ncclMax, comm->ctl,
+                                      comm->ctl_stream);
+  if (nr != ncclSuccess) return abort_comm(comm, nccl_fail(comm, nr));
+  if ((e = hipMemcpyAsync(comm->h_status + 1, comm->d_status, 4, hipMemcpyDeviceToHost, comm->ctl_stream)) !=
+      hipSuccess) {
+    ufc_internal::note_hip_error(comm->ctx, (int)e);
+    return abort_comm(comm, UFC_ERR_HIP);
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; spin++) {
+    e = hipStreamQuery(comm->ctl_stream);
+    if (e == hipSuccess) break;
+    if (e != hipErrorNotReady) {
+      ufc_internal::note_hip_error(comm->ctx, (int)e);
+      return abort_comm(comm, UFC_ERR_HIP);
+    }
+    ncclResult_t ae = ncclSuccess;
+    if (r.CommGetAsyncError(comm->ctl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
+      return abort_comm(comm, nccl_fail(comm, ae));
+    const auto waited = std::chrono::steady_clock::now() - t0;
+    if (comm->timeout_ms > 0 && waited > std::chrono::milliseconds(comm->timeout_ms))
+      return abort_comm(comm, UFC_ERR_TIMEOUT);
+    if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(spin > 20000 ? 1000 : 20));
+  }
+  if (local_rc != UFC_OK) return local_rc;
+  return comm->h_status[1] != 0 ? UFC_ERR_PEER : UFC_OK;
 }
 
 // The gate of one chunk's frames, results into the rank's outputs at `dst`.
@@ -341,11 +402,26 @@ int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const ui
       return UFC_ERR_HIP;
     }
   }
+  hipError_t he = hipStreamCreateWithFlags(&c->ctl_stream, hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipMalloc(&c->d_status, 4);
+  if (he == hipSuccess) he = hipHostMalloc(&c->h_status, 8, hipHostMallocDefault);
+  if (he != hipSuccess) {
+    ufc_internal::note_hip_error(ctx, (int)he);
+    ufc_comm_destroy(c);
+    return UFC_ERR_HIP;
+  }
   ncclUniqueId u;
   std::memcpy(&u, id, sizeof u);
-  const ncclResult_t nr = r.CommInitRank(&c->nccl, nranks, u, rank);  // collective over the ranks
+  ncclResult_t nr = r.CommInitRank(&c->nccl, nranks, u, rank);  // collective over the ranks
   if (nr != ncclSuccess) {
     c->nccl = nullptr;
+    c->last_nccl_error = (int)nr;
+    ufc_comm_destroy(c);
+    return UFC_ERR_COMM;
+  }
+  if ((nr = r.CommSplit(c->nccl, 0, rank, &c->ctl, nullptr)) != ncclSuccess) {  // collective too
+    c->ctl = nullptr;
+    c->last_nccl_error = (int)nr;
     ufc_comm_destroy(c);
     return UFC_ERR_COMM;
   }
@@ -357,15 +433,25 @@ int ufc_comm_destroy(ufc_comm* comm) {
   if (!comm) return UFC_OK;
   {
     DeviceGuard g(ufc_internal::ctx_device(comm->ctx));
+    if (comm->ctl) (void)rccl().CommDestroy(comm->ctl);
     if (comm->nccl) (void)rccl().CommDestroy(comm->nccl);
     for (hipEvent_t& e : comm->ev)
       if (e) (void)hipEventDestroy(e);
+    if (comm->ctl_stream) (void)hipStreamDestroy(comm->ctl_stream);
+    if (comm->d_status) (void)hipFree(comm->d_status);
+    if (comm->h_status) (void)hipHostFree(comm->h_status);
   }
   delete comm;
   return UFC_OK;
 }
 
 int ufc_comm_last_error(const ufc_comm* comm) { return comm ? comm->last_nccl_error : 0; }
+
+int ufc_comm_set_timeout(ufc_comm* comm, int timeout_ms) {
+  if (!comm || timeout_ms < 0) return UFC_ERR_INVALID_ARG;
+  comm->timeout_ms = timeout_ms;
+  return UFC_OK;
+}
 
 int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size_t frame_len, uint64_t n_total,
                     uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream) {
@@ -374,9 +460,9 @@ int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size
   uint64_t bounds[UFC_MAX_RANKS + 1];
   (void)ufc_shard_bounds_fixed(n_total, comm->nranks, bounds);
   const uint64_t cnt = bounds[comm->rank + 1] - bounds[comm->rank];
-  // Rank-local: this rank's frames.  Fails before any transfer here, but the peers' transfers to or
-  // from this rank then stall: abort, so the failure is visible (ufc_comm_last_error / broken).
-  if (cnt && !d_frames) return comm->nranks > 1 ? abort_comm(comm, UFC_ERR_INVALID_ARG) : UFC_ERR_INVALID_ARG;
+  // Rank-local: this rank's frames.  Agreed with the peers before any transfer, so the call fails on
+  // every rank (UFC_ERR_PEER on the others) and nothing is left queued.
+  if (const int rc = agree_status(comm, cnt && !d_frames ? UFC_ERR_INVALID_ARG : UFC_OK)) return rc;
   const FixedArgs args{comm->ctx, d_frames, stride, frame_len};
   hipStream_t s = (hipStream_t)stream;
   return run_sharded(comm, bounds, gate_fixed, &args, d_crc_out, d_valid_out, root, s,
@@ -388,8 +474,7 @@ int ufc_crc_sharded_varlen(ufc_comm* comm, const uint8_t* d_bytes, const uint64_
   if (const int rc = check_common(comm, root, d_crc_out || d_valid_out)) return rc;
   if (!bounds_ok(bounds, comm->nranks)) return UFC_ERR_INVALID_ARG;
   const uint64_t cnt = bounds[comm->rank + 1] - bounds[comm->rank];
-  if (cnt && (!d_bytes || !d_offsets))
-    return comm->nranks > 1 ? abort_comm(comm, UFC_ERR_INVALID_ARG) : UFC_ERR_INVALID_ARG;
+  if (const int rc = agree_status(comm, cnt && (!d_bytes || !d_offsets) ? UFC_ERR_INVALID_ARG : UFC_OK)) return rc;
   const VarlenArgs args{comm->ctx, d_bytes, d_offsets};
   hipStream_t s = (hipStream_t)stream;
   return run_sharded(comm, bounds, gate_varlen, &args, d_crc_out, d_valid_out, root, s,
