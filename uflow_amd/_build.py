@@ -41,11 +41,23 @@ def _digest(paths, extra=()):
 
 
 def _stamp_ok(target, digest):
+    """Whether <target>.sha256 records `digest` (its first line)."""
     try:
         with open(target + ".sha256") as f:
-            return os.path.exists(target) and f.read().strip() == digest
+            return os.path.exists(target) and f.readline().strip() == digest
     except OSError:
         return False
+
+
+def _stamp_defines(target):
+    """The -D defines recorded in <target>.sha256 (second line, "defines: A B=1 ..."), or ()."""
+    try:
+        with open(target + ".sha256") as f:
+            f.readline()
+            line = f.readline().strip()
+    except OSError:
+        return ()
+    return tuple(line[len("defines:"):].split()) if line.startswith("defines:") else ()
 
 
 def _native_identity(tuning=False, defines=()):
@@ -64,8 +76,9 @@ def _native_identity(tuning=False, defines=()):
 
 
 def tuning_lib_current(path):
-    """Whether the tuning library at `path` was built from this tree's sources (its stamp)."""
-    return _stamp_ok(path, _native_identity(tuning=True)[2])
+    """Whether the tuning library at `path` was built from this tree's sources (its stamp), with the
+    -D defines its stamp records (ablation builds)."""
+    return _stamp_ok(path, _native_identity(tuning=True, defines=_stamp_defines(path))[2])
 
 
 def build_native(force=False, verbose=False, tuning=False, out=None, defines=()):
@@ -105,6 +118,8 @@ def build_native(force=False, verbose=False, tuning=False, out=None, defines=())
     os.replace(target + ".tmp", target)
     with open(target + ".sha256", "w") as f:
         f.write(digest + "\n")
+        if defines:
+            f.write("defines: " + " ".join(defines) + "\n")
     return target
 
 

@@ -43,6 +43,12 @@ enum : uint8_t { kItemsNone = 0, kItemsPos = 1, kItemsAck = 2, kItemsWalk = 3 };
 
 typedef hipcub::BlockScan<uint32_t, kParseThreads> BlockScan;
 
+// Byte-aligned global views: the IR carries align 1, so the compiler never assumes 4- or 8-byte
+// alignment when it combines or splits these loads; gfx950's unaligned access mode still makes each
+// one a single global_load_dword / dwordx2.
+typedef const __attribute__((address_space(1), aligned(1))) uint32_t g_u32_a1;
+typedef const __attribute__((address_space(1), aligned(1))) uint64_t g_u64_a1;
+
 struct DevBytes {
   const uint8_t* p;
   __device__ uint32_t operator()(uint32_t i) const {
@@ -51,7 +57,7 @@ struct DevBytes {
   // one dword load at any byte address (gfx950's unaligned access mode; the codec guarantees the
   // four bytes lie inside the frame): one round trip and one address pass for a datagram's sizes
   __device__ uint32_t head3(uint32_t i) const {
-    return *(const __attribute__((address_space(1))) uint32_t*)(p + i) & 0xFFFFFFu;
+    return *(g_u32_a1*)(p + i) & 0xFFFFFFu;
   }
 };
 
@@ -62,14 +68,14 @@ struct DevBytesHead {
   uint64_t w;  // bytes 0..7, little-endian
   bool has8;
   __device__ static uint64_t load8(const uint8_t* q) {  // (any byte address: unaligned access mode)
-    return *(const __attribute__((address_space(1))) uint64_t*)q;
+    return *(g_u64_a1*)q;
   }
   __device__ uint32_t operator()(uint32_t i) const {
     if (has8 && i < 8) return (uint32_t)(w >> (8 * i)) & 0xFFu;
     return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
   }
   __device__ uint32_t head3(uint32_t i) const {
-    return *(const __attribute__((address_space(1))) uint32_t*)(p + i) & 0xFFFFFFu;
+    return *(g_u32_a1*)(p + i) & 0xFFFFFFu;
   }
 };
 
@@ -117,7 +123,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
                                                                    uint64_t n, const uint8_t* valid,
                                                                    ufc_frame_info* infos, uint32_t* counts,
                                                                    uint8_t* modes, uint16_t* pos_seg,
-                                                                   uint32_t* seg_cursor, uint32_t* seg_base,
+                                                                   unsigned long long* seg_cursor, uint32_t* seg_base,
                                                                    uint64_t seg_cap) {
   __shared__ uint16_t slots[kSegWords];
   __shared__ typename BlockScan::TempStorage scan_tmp;
@@ -152,8 +158,9 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
   // the workgroup's segment of header slots, from the launch's bump counter (no room: the emit
   // step re-walks this workgroup's frames instead)
   if (t == 0) {
-    uint32_t b = total ? atomicAdd(seg_cursor, total) : 0u;
-    if (total && (uint64_t)b + total > seg_cap) b = 0xFFFFFFFFu;
+    // (64-bit cursor: the sum of every workgroup's total may pass 2^32 long after the cap is reached)
+    const unsigned long long b64 = total ? atomicAdd(seg_cursor, (unsigned long long)total) : 0ull;
+    const uint32_t b = (total && b64 + total > seg_cap) ? 0xFFFFFFFFu : (uint32_t)b64;
     base_lds = b;
     seg_base[blockIdx.x] = b;
   }
@@ -210,7 +217,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
                                                                         uint64_t n, const uint8_t* valid,
                                                                         ufc_frame_info* infos, uint32_t* counts,
                                                                         uint8_t* modes, uint16_t* pos_seg,
-                                                                        uint32_t* seg_cursor, uint32_t* seg_base,
+                                                                        unsigned long long* seg_cursor, uint32_t* seg_base,
                                                                         uint64_t seg_cap) {
   __shared__ uint16_t slots[kInlineSlots * kParseThreads];
   __shared__ uint32_t pool[kPoolSlots];
@@ -249,8 +256,9 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   uint32_t lo, total;
   BlockScan(scan_tmp).ExclusiveSum(npos, lo, total);
   if (t == 0) {
-    uint32_t b = total ? atomicAdd(seg_cursor, total) : 0u;
-    if (total && (uint64_t)b + total > seg_cap) b = 0xFFFFFFFFu;
+    // (64-bit cursor: the sum of every workgroup's total may pass 2^32 long after the cap is reached)
+    const unsigned long long b64 = total ? atomicAdd(seg_cursor, (unsigned long long)total) : 0ull;
+    const uint32_t b = (total && b64 + total > seg_cap) ? 0xFFFFFFFFu : (uint32_t)b64;
     base_lds = b;
     seg_base[blockIdx.x] = b;
   }
@@ -416,7 +424,10 @@ struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned pa
   ParseLayout(uint64_t n, uint64_t items_cap, size_t temp_bytes) {
     auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
     const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
-    seg_cap = std::min<uint64_t>(n * kPosSlots, std::max<uint64_t>(items_cap, 1));  // u16 header slots
+    // u16 header slots; below 2^32 - 1 so that every segment fits 32-bit offsets and no segment base
+    // can equal the overflow sentinel 0xFFFFFFFF (frames past the cap are walked again, kItemsWalk)
+    seg_cap = std::min<uint64_t>(std::min<uint64_t>(n * kPosSlots, std::max<uint64_t>(items_cap, 1)),
+                                 0xFFFFFFFEull - kSegWords);
     counts = 0;
     firsts = counts + up(n * 4);
     modes = firsts + up(n * 4);
@@ -447,12 +458,12 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   uint32_t* counts = (uint32_t*)(s + lay.counts);
   uint32_t* firsts = (uint32_t*)(s + lay.firsts);
   uint8_t* modes = (uint8_t*)(s + lay.modes);
-  uint32_t* cursor = (uint32_t*)(s + lay.cursor);
+  unsigned long long* cursor = (unsigned long long*)(s + lay.cursor);
   uint32_t* bases = (uint32_t*)(s + lay.bases);
   uint16_t* pos_seg = (uint16_t*)(s + lay.slots);
   void* temp = s + lay.temp;
   size_t temp_bytes = lay.end - lay.temp;
-  hipError_t e = hipMemsetAsync(cursor, 0, 4, stream);
+  hipError_t e = hipMemsetAsync(cursor, 0, 8, stream);
   if (e != hipSuccess) return e;
   bool pool = true;  // pooled header slots (more walking frames per CU); UFC_WALK_POOL=0 (tuning): fixed slots
 #ifdef UFC_TUNING

@@ -609,27 +609,31 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
 int ufc_ctx_release_stream(ufc_ctx* ctx, void* stream) {
   if (!ctx) return UFC_ERR_INVALID_ARG;
   DeviceGuard g(ctx->device);
-  std::lock_guard<std::mutex> lk(ctx->scratch_mu);
-  bool synced = false;
-  int rc = UFC_OK;
-  for (size_t i = 0; i < ctx->scratch.size();) {
-    ufc_ctx::Scratch& sc = ctx->scratch[i];
-    if (sc.stream != (hipStream_t)stream) {
-      i++;
-      continue;
-    }
-    if (!synced) {  // the work queued on the stream may still use its scratch
-      const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
-      if (e != hipSuccess) {
-        rc = hip_fail(ctx, e);
-        break;
-      }
-      synced = true;
-    }
-    if (sc.p) (void)hipFree(sc.p);
-    ctx->scratch.erase(ctx->scratch.begin() + (long)i);
+  bool any = false;
+  {
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    for (const auto& sc : ctx->scratch) any = any || sc.stream == (hipStream_t)stream;
   }
-  return rc;
+  if (!any) return UFC_OK;
+  // The work queued on the stream may still use its scratch: wait for it without holding the lock,
+  // so that scratch lookups of other streams go on meanwhile (the caller is retiring this stream and
+  // queues nothing more on it).
+  const hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(ctx, e);
+  std::vector<void*> dead;
+  {
+    std::lock_guard<std::mutex> lk(ctx->scratch_mu);
+    for (size_t i = 0; i < ctx->scratch.size();) {
+      if (ctx->scratch[i].stream != (hipStream_t)stream) {
+        i++;
+        continue;
+      }
+      if (ctx->scratch[i].p) dead.push_back(ctx->scratch[i].p);
+      ctx->scratch.erase(ctx->scratch.begin() + (long)i);
+    }
+  }
+  for (void* p : dead) (void)hipFree(p);
+  return UFC_OK;
 }
 
 int ufc_ctx_destroy(ufc_ctx* ctx) {
