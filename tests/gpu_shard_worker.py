@@ -153,15 +153,21 @@ def timeout_main():
     code = 0
     if rank != 0:
         dist.barrier()  # after rank 0 has timed out
+    def note(msg):  # progress on stderr: a hang names its step
+        print(f"[timeout worker rank {rank}] {msg}", file=sys.stderr, flush=True)
+
+    note("calling crc_sharded")
     t0 = time.monotonic()
     try:
         gate.crc_sharded(frames, L, total, crc, None, root=0)
     except NativeError as e:
         code = e.code
     waited = time.monotonic() - t0
+    note(f"returned {code} after {waited:.2f} s")
     if rank == 0:
         dist.barrier()
     gate.close()  # destroy after abort
+    note("communicator destroyed")
     codes = torch.zeros(world, dtype=torch.int32, device=dev)
     codes[rank] = code
     dist.all_reduce(codes)

@@ -31,9 +31,14 @@ L = 1500
 FULL_LAUNCH = 4_186_112  # 256 CUs x 8 waves x 511 sets x 4 frames (ufc_api.cpp launch_lean_fixed)
 
 
-def _first_diff(a, b):
-    ne = torch.nonzero(a != b)
-    return int(ne[0]) if ne.numel() else -1
+def _first_diff(a, b, chunk=1 << 28):
+    """First index where two equal-length uint8 device tensors differ, or -1 (chunked: one
+    nonzero over several GB of bytes overflows its workspace)."""
+    for c0 in range(0, a.numel(), chunk):
+        x, y = a[c0:c0 + chunk], b[c0:c0 + chunk]
+        if not torch.equal(x, y):
+            return c0 + int(torch.nonzero(x != y)[0])
+    return -1
 
 
 def test_ramp_sequence_vs_oracle(engine):
@@ -56,7 +61,7 @@ def test_ramp_sequence_vs_oracle(engine):
             torch.cuda.synchronize()
             k = _first_diff(d[:n * L], ref[:n * L])
             assert k < 0, f"seal n={n} crc_out={with_crc}: first differing byte {k} (frame {k // L})"
-            assert torch.equal(d[n * L:], raw[n * L:]), f"seal n={n} wrote past its frames"
+            assert _first_diff(d[n * L:], raw[n * L:]) < 0, f"seal n={n} wrote past its frames"
             if with_crc:
                 got = crc_out.cpu().numpy().view(np.uint32)
                 assert np.array_equal(got, ref_crc[:n]), f"seal n={n}: crc_out differs"

@@ -11,6 +11,7 @@ The plan itself is checked in C (tests/c/c_abi_smoke.c) and executed over gloo (
 import json
 import re
 import os
+import signal
 import socket
 import subprocess
 import sys
@@ -96,7 +97,16 @@ def _run_worker(world, args, timeout):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
            os.path.join(repo, "tests", "gpu_shard_worker.py")] + args
-    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=repo)
+    # own process group: on a timeout the launcher AND its ranks are killed (no orphan keeps the GPU)
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=repo,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        out, err = p.communicate()
+        pytest.fail(f"ranks did not finish in {timeout} s; stdout tail: {out[-1500:]}; stderr tail: {err[-3000:]}")
+    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -127,7 +137,7 @@ def test_sharded_peer_timeout():
     """ufc_comm_set_timeout: rank 0 of 2 calls alone and gets UFC_ERR_TIMEOUT (-7) after its 3 s
     deadline (communicator aborted); rank 1 calls afterwards and fails too; both destroy their
     aborted communicators (tests/gpu_shard_worker.py --timeout)."""
-    p = _run_worker(2, ["--timeout"], 180)
+    p = _run_worker(2, ["--timeout"], 90)
     assert p.returncode == 0, p.stderr[-3000:]
     j = json.loads(re.findall(r"\{[^{}]*\}", p.stdout)[0])
     assert j["timeout_codes"][0] == -7, j

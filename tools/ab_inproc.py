@@ -105,6 +105,7 @@ def main():
         assert r == 0
 
     times = {v[0]: [] for v in variants}
+    first_out = [None]
     for rnd in range(rounds):
         for name, path, env in variants:
             saved = {k: os.environ.get(k) for k in env}
@@ -123,7 +124,13 @@ def main():
                 print(f"# {name} round {rnd}: " + " ".join(f"{t:.3f}" for t in ts), flush=True)
             if rnd == 0 and "UFC_LEAN_ABL" not in env and "UFC_VL_ABL" not in env and "UFC_ABLATE" not in env:
                 nv = int(valid.sum().item())
-                print(f"# {name}: valid {nv} of {n}", flush=True)
+                same = ""
+                if first_out[0] is None:
+                    first_out[0] = (name, crc.clone(), valid.clone())
+                else:
+                    same = (f"; crc words and flags identical to {first_out[0][0]}'s: "
+                            f"{bool(torch.equal(crc, first_out[0][1]) and torch.equal(valid, first_out[0][2]))}")
+                print(f"# {name}: valid {nv} of {n}{same}", flush=True)
             for k, v in saved.items():
                 if v is None:
                     del os.environ[k]

@@ -80,7 +80,8 @@ const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // runs sorted inside the kernel from the CSR offsets / pairs in p.offsets (product); otherwise
 // p.offsets = sort_runs records (tuning builds only, A/B).  Pairs need the buffer below
 // 2^31 - 2^20 bytes (32-bit offsets from the buffer).
-const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw = 64, int aux = 0);
+// geor: each run's geometry computed once per frame before the sort (GEOR in frame_crc_varlen8.hip).
+const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw = 64, int aux = 0, bool geor = false);
 // Byte-balanced streaming kernel (frame_crc_varlen8.hip): CSR batches, 12 waves per workgroup, one
 // workgroup per CU; tables as the 8-lane kernel (A^128 chains, the 32-slot nibble image).  A launch
 // covers fewer than 2^31 frames.

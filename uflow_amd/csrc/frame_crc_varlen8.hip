@@ -183,9 +183,16 @@ struct Buf8 {
 // CSR offsets (nullptr for pairs: p.frame_len = the buffer length, relative offsets < 2^31).
 // SORTW: runs are ordered by block count within aligned windows of SORTW frames (64: the whole run;
 // 8: no reordering across sets, i.e. each set is 8 consecutive frames).
-template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux>
+// GEOR (with INSORT): each run's geometry is computed once per frame, in the frame's own lane,
+// before the sort (one frame per lane instead of once per set in each of a group's 8 lanes), and
+// the per-set facts (max block count, mixed counts, byte path, G in block 1) once per run with
+// half-row DPP reductions and ballots; a set then takes its two words per group with ds_bpermute
+// and its set-level bits with one readfirstlane.  Frames the fast path cannot take sort together
+// (key 7), so they spoil fewer sets.
+template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux, bool GEOR = false>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
   static_assert(SORTW == 8 || SORTW == 16 || SORTW == 32 || SORTW == 64, "sort window");
+  static_assert(!GEOR || INSORT, "per-run geometry needs the in-kernel sort");
   constexpr int JM = kV8Blocks;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
 #ifdef UFC_TUNING
@@ -229,13 +236,50 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     a = *as_global<g_u64>(offs + (PAIRS ? 2 * fi : fi));
     b = *as_global<g_u64>(offs + (PAIRS ? 2 * fi + 1 : fi + 1));
   };
-  auto sort_run = [&](uint32_t r, uint64_t a, uint64_t b, SRec& out) {
+  const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets_csr + nfr);
+  const bool flat = PAIRS && p.frame_len < (1ull << 31) - (1ull << 20);
+  // GEOR: the fast-path geometry of this lane's frame (unsorted), relative to the run's base sb
+  // (the run's first frame, or the buffer itself for flat pairs, minus the bias; wave-uniform).
+  struct FGeo {
+    uint32_t geo, wrel;
+    bool bad;
+  };
+  auto frame_geo = [&](uint64_t a, uint64_t len64, bool live, uint64_t sb) -> FGeo {
+    const uint32_t len = (uint32_t)min(len64, (uint64_t)0x40000000u);  // (longer: J > 6, the byte path)
+    const uint32_t t = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a + len)) & 3u;  // end up to 4 B
+    const uint32_t J = (len + t + 4u + 255u) >> 8;
+    const uint32_t pad = (J * 256u - len - t) & 511u;
+    const uint64_t rel64 = a - sb;
+    FGeo g;
+    g.wrel = (uint32_t)rel64 - pad;  // window start (4-byte aligned)
+    g.bad = !live || len < 4u || J > (uint32_t)JM || a < (uint64_t)pad || a + len + 3 > buf_end ||
+            rel64 >= (uint64_t)kV8Limit || rel64 < 512u;
+    g.geo = pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | (L.lane << 16) |
+            ((live ? 0u : 1u) << 22) | ((g.bad ? 1u : 0u) << 23);
+    return g;
+  };
+  auto run_base = [&](uint64_t a) -> uint64_t {
+    const uint64_t b0 = flat ? 0u : (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a) |
+                                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a >> 32)) << 32)) &
+                                     ~3ull);
+    return b0 - kV8Bias;
+  };
+  // RAW: permute the raw record (a, len, lane | dead) even in GEOR mode (the byte path's re-sort:
+  // the same keys, so the same permutation).
+  auto sort_run = [&](uint32_t r, uint64_t a, uint64_t b, SRec& out, bool raw = false) {
     const uint64_t f = (uint64_t)r * kRunFrames + L.lane;
     const bool live = r != kNoSet && f < nfr;
     const uint64_t len = (live && b >= a) ? b - a : 0u;
     const uint64_t n4 = len >= 4 ? len - 4 : len;
     const uint64_t J = (n4 + 8 + 255) >> 8;
-    const uint32_t key = !live ? 8u : ((len >= 4 && len < 0x40000000ull && J <= (uint64_t)JM) ? (uint32_t)J : 7u);
+    uint32_t key = !live ? 8u : ((len >= 4 && len < 0x40000000ull && J <= (uint64_t)JM) ? (uint32_t)J : 7u);
+    FGeo fg{0u, 0u, false};
+    uint64_t sb = 0;
+    if constexpr (GEOR) {
+      sb = run_base(a);
+      fg = frame_geo(a, len, live, sb);
+      key = !live ? 8u : (fg.bad ? 7u : (uint32_t)J);
+    }
     if constexpr (SORTW == 8) {  // sets of consecutive frames: no reordering
       out.a_lo = (uint32_t)a;
       out.a_hi = (uint32_t)(a >> 32);
@@ -253,13 +297,39 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       rank_in = (k == key) ? rk : rank_in;
     }
     const int dst = (int)(((L.lane & ~(uint32_t)(SORTW - 1)) + below + rank_in) * 4u);
+    if constexpr (GEOR) {
+      if (!raw) {
+        // lane = sorted position: per-set facts over each 8-lane half-row, packed into geo bits 24..29
+        uint32_t geo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.geo);
+        out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.wrel);
+        out.len = (uint32_t)sb;
+        out.info = (uint32_t)(sb >> 32);
+        const uint32_t Jk = (geo >> 9) & 7u;
+        uint32_t jx = Jk, jn = Jk;
+        jx = max(jx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jx, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+        jn = min(jn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jn, 0xB1, 0xF, 0xF, false));
+        jx = max(jx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jx, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+        jn = min(jn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jn, 0x4E, 0xF, 0xF, false));
+        jx = max(jx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jx, 0x141, 0xF, 0xF, false));  // row_half_mirror
+        jn = min(jn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jn, 0x141, 0xF, 0xF, false));
+        const uint64_t mbad = __builtin_amdgcn_ballot_w64(((geo >> 23) & 1u) != 0);
+        const uint64_t mg1 = __builtin_amdgcn_ballot_w64((geo & 511u) > 256u);
+        const uint32_t s8 = L.lane & ~7u;
+        const uint32_t slow = ((mbad >> s8) & 0xFFu) != 0 ? 1u : 0u, g1 = ((mg1 >> s8) & 0xFFu) != 0 ? 1u : 0u;
+        out.a_lo = geo | (min(jx, (uint32_t)JM) << 24) | ((jx != jn ? 1u : 0u) << 27) | (slow << 28) | (g1 << 29);
+        return;
+      }
+    }
     out.a_lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)a);
     out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(a >> 32));
     out.len = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)min(len, (uint64_t)0xFFFFFFFFu));
     out.info = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(L.lane | (live ? 0u : 0x80000000u)));
   };
-  auto take_rec = [&](const SRec& sr, uint32_t q) -> uint4 {
+  auto take_rec = [&](const SRec& sr, uint32_t q, bool raw = false) -> uint4 {
     const int src = (int)(((q & 7u) * 8u + L.grp) * 4u);
+    if (GEOR && !raw)
+      return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_lo),
+                        (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_hi), sr.len, sr.info);
     return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_lo),
                       (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_hi),
                       (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.len),
@@ -300,7 +370,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
   if constexpr (INSORT) sort_run(run, a0, b0, SR);
   const uint4* rec = (const uint4*)p.offsets;
-  const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets_csr + nfr);
 
   // This group's record of set q (the same 16 bytes in the group's 8 lanes).
   auto load_rec = [&](uint32_t q) -> uint4 {
@@ -313,8 +382,19 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   // offset, meta, and the set's base (buffer offset of its loads' resource, minus a bias): its
   // group-0 frame's start (CSR: the fast frames of a run lie within 64 x 1.5 KB of each other),
   // or the buffer itself for pairs over less than 2 GB (pairs may come in any order).
-  const bool flat = PAIRS && p.frame_len < (1ull << 31) - (1ull << 20);
   auto geometry = [&](uint32_t q, uint4 r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
+    if constexpr (GEOR) {  // r = (geo | set bits, window start, run base lo, hi) from the run's sort
+      sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.z) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.w) << 32);
+      const uint32_t gu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.x);
+      m.Jset = (gu >> 24) & 7u;
+      m.mixed = ((gu >> 27) & 1u) != 0;
+      m.slow = ((gu >> 28) & 1u) != 0;
+      m.g1 = ((gu >> 29) & 1u) != 0;
+      const bool live = q != kNoSet && !m.slow;
+      voff0 = live ? r.y + 16u * L.col : kV8Oob;
+      return r.x & 0x7FFFFFu;
+    }
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const uint32_t len = min(r.z, 0x40000000u);  // (longer: J > 6, the byte path)
     const bool dead = (r.w >> 31) != 0;
@@ -431,8 +511,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       uint64_t a, b;
       SRec T;
       raw_load(q >> 3, a, b);
-      sort_run(q >> 3, a, b, T);
-      r = take_rec(T, q);
+      sort_run(q >> 3, a, b, T, true);
+      r = take_rec(T, q, true);
     } else {
       r = load_rec(q);
     }
@@ -582,10 +662,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   template __global__ void frame_crc_varlen8_kernel<SEAL, false, 12, 2, true, SW>(const KernelParams);
 #define UFC_V8_INSTA(SW) \
   template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, SW, 2>(const KernelParams);
+#define UFC_V8_INSTG(SEAL, PAIRS) \
+  template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, 12, 2, true, 64, kV8Aux, true>(const KernelParams);
 // Product: 12 waves, 2 sets per wave in the ring (three waves per SIMD; config 3 1.69 ms kernel
 // against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill), runs sorted
 // in the kernel.  The pre-sorted variant (records from sort_runs) is kept for A/B in tuning builds.
 UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
+UFC_V8_INSTG(false, false) UFC_V8_INSTG(true, false) UFC_V8_INSTG(false, true) UFC_V8_INSTG(true, true)
 #ifdef UFC_TUNING
 UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
 UFC_V8_INSTW(false, 8) UFC_V8_INSTW(false, 16) UFC_V8_INSTW(false, 32) UFC_V8_INSTW(true, 8) UFC_V8_INSTW(true, 16)
@@ -594,6 +677,7 @@ UFC_V8_INSTW(true, 32) UFC_V8_INSTA(8) UFC_V8_INSTA(16) UFC_V8_INSTA(32) UFC_V8_
 #undef UFC_V8_INST
 #undef UFC_V8_INSTW
 #undef UFC_V8_INSTA
+#undef UFC_V8_INSTG
 
 // =============================================================================================
 // Byte-balanced streaming kernel (round 3, SURVEY.md section 7 step 6: "one byte stream"): CSR
@@ -979,7 +1063,15 @@ const void* stream8_kernel_symbol(bool seal) {
 #endif
 }
 
-const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux) {
+const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux, bool geor) {
+  if (geor) {
+    if (!insort || sortw != 64 || aux != kV8Aux) return nullptr;
+    if (pairs)
+      return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true, 64, kV8Aux, true>
+                  : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, true, 64, kV8Aux, true>;
+    return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8Aux, true>
+                : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8Aux, true>;
+  }
 #ifdef UFC_TUNING
   if (insort && !pairs && !seal && aux == 2) {  // A/B: non-temporal loads (CSR validate)
     switch (sortw) {

@@ -334,11 +334,13 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
 #endif
   const int waves = 12;
   int sortw = 64, aux = 0;  // runs sorted whole, default-policy loads; UFC_V8_SORTW / UFC_V8_AUX (tuning): A/B
+  bool geor = false;        // per-run geometry (UFC_V8_GEOR, tuning A/B)
 #ifdef UFC_TUNING
   if (const char* sw = std::getenv("UFC_V8_SORTW")) sortw = std::atoi(sw);
   if (const char* ax = std::getenv("UFC_V8_AUX")) aux = std::atoi(ax);
+  if (const char* gr = std::getenv("UFC_V8_GEOR")) geor = std::atoi(gr) != 0;
 #endif
-  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, insort, sortw, aux);
+  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, insort, sortw, aux, geor);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain128;
   kp.nib_img = ctx->d_nib32;

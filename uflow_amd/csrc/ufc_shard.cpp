@@ -425,6 +425,27 @@ int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const ui
     ufc_comm_destroy(c);
     return UFC_ERR_COMM;
   }
+  // Connect the control communicator now, while every rank is here: RCCL sets a communicator's
+  // connections up at its first collective, inside the enqueueing call and blocking the host until
+  // the peers join.  Left to the first agree_status, a rank calling alone would block there, before
+  // its deadline is ever checked; connected, the all-reduce only enqueues and the deadline applies.
+  if (nranks > 1) {
+    c->h_status[0] = 0;
+    he = hipMemcpyAsync(c->d_status, c->h_status, 4, hipMemcpyHostToDevice, c->ctl_stream);
+    if (he == hipSuccess) {
+      if ((nr = r.AllReduce(c->d_status, c->d_status, 1, ncclInt32, ncclMax, c->ctl, c->ctl_stream)) != ncclSuccess) {
+        c->last_nccl_error = (int)nr;
+        ufc_comm_destroy(c);
+        return UFC_ERR_COMM;
+      }
+      he = hipStreamSynchronize(c->ctl_stream);
+    }
+    if (he != hipSuccess) {
+      ufc_internal::note_hip_error(ctx, (int)he);
+      ufc_comm_destroy(c);
+      return UFC_ERR_HIP;
+    }
+  }
   *out = c;
   return UFC_OK;
 }
