@@ -3,8 +3,8 @@
 - World size 1 in this process: the RCCL communicator is created through the library's own
   binding, the shard is gated chunk by chunk (front-readable chunks after the first), results land
   in their global positions, and every frame matches the oracle.
-- World sizes 2 and 3 on the one GPU of the test box (tests/gpu_shard_worker.py under
-  torch.distributed.run): RCCL's socket transport stands in for xGMI, so the senders' ncclSend and
+- World sizes 2 and 3 on the one GPU of the test box (tests/gpu_shard_worker.py, one process per
+  rank, env:// rendezvous): RCCL's socket transport stands in for xGMI, so the senders' ncclSend and
   the root's ncclRecv into global frame order run for real; every gathered word is checked.
 The plan itself is checked in C (tests/c/c_abi_smoke.c) and executed over gloo (test_shard_gloo.py).
 """
@@ -14,6 +14,8 @@ import os
 import signal
 import socket
 import subprocess
+import time
+import tempfile
 import sys
 
 import numpy as np
@@ -88,25 +90,52 @@ def test_sharded_varlen_world1_config3(engine, gate):
 
 
 def _run_worker(world, args, timeout):
+    """`world` ranks of tests/gpu_shard_worker.py started directly (env:// rendezvous on 127.0.0.1),
+    each in a process group of its own with its output in a file: on a timeout every rank's group is
+    killed and the output read so far names the step that hung."""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port),
-           os.path.join(repo, "tests", "gpu_shard_worker.py")] + args
-    # own process group: on a timeout the launcher AND its ranks are killed (no orphan keeps the GPU)
-    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env, cwd=repo,
-                         start_new_session=True)
-    try:
-        out, err = p.communicate(timeout=timeout)
-    except subprocess.TimeoutExpired:
-        os.killpg(p.pid, signal.SIGKILL)
-        out, err = p.communicate()
-        pytest.fail(f"ranks did not finish in {timeout} s; stdout tail: {out[-1500:]}; stderr tail: {err[-3000:]}")
-    return subprocess.CompletedProcess(cmd, p.returncode, out, err)
+    base = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    cmd = [sys.executable, os.path.join(repo, "tests", "gpu_shard_worker.py")] + args
+    procs, files = [], []
+    for r in range(world):
+        env = dict(base, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0")
+        fo, fe = tempfile.TemporaryFile("w+"), tempfile.TemporaryFile("w+")
+        files.append((fo, fe))
+        procs.append(subprocess.Popen(cmd, stdout=fo, stderr=fe, text=True, env=env, cwd=repo, start_new_session=True))
+    deadline = time.monotonic() + timeout
+    timed_out = False
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, deadline - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            timed_out = True
+            break
+    if timed_out:
+        for p in procs:
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+        for p in procs:
+            p.wait()
+    outs, errs = [], []
+    for fo, fe in files:
+        fo.seek(0)
+        fe.seek(0)
+        outs.append(fo.read())
+        errs.append(fe.read())
+        fo.close()
+        fe.close()
+    out, err = "".join(outs), "\n".join(f"--- rank {r} ---\n{e[-2000:]}" for r, e in enumerate(errs))
+    if timed_out:
+        pytest.fail(f"ranks did not finish in {timeout} s; stdout: {out[-1500:]}; stderr: {err}")
+    rc = max((p.returncode for p in procs), key=abs)
+    return subprocess.CompletedProcess(cmd, rc, out, err)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -106,6 +106,13 @@ def main():
 
     times = {v[0]: [] for v in variants}
     first_out = [None]
+    # settle: a GPU out of idle runs at reduced clocks for up to ~1 s (AB_SETTLE_MS)
+    import time
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < float(os.environ.get("AB_SETTLE_MS", 1500)):
+        for name, path, env in variants:
+            launch(*libs[name])
+        torch.cuda.synchronize()
     for rnd in range(rounds):
         for name, path, env in variants:
             saved = {k: os.environ.get(k) for k in env}

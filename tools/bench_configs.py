@@ -62,7 +62,8 @@ def ceiling(eng, buf, reps):
     return round(nbytes / med / 1e-3 / 1e9, 1)
 
 
-def settle(fn, ms=50):
+def settle(fn, ms=1000):
+    """Launches for `ms` before timing: a GPU out of idle runs at reduced clocks for up to ~1 s."""
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < ms:
         fn()

@@ -20,8 +20,11 @@ valid = torch.empty(n, dtype=torch.uint8, device="cuda")
 
 
 def timeit(fn, reps=40):
-    for _ in range(10):
+    import time
+    t0 = time.perf_counter()  # settle: clocks ramp up from idle over ~1 s
+    while time.perf_counter() - t0 < 1.5:
         fn()
+        torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
     for a, b in ev:
         a.record()

@@ -42,11 +42,13 @@ def timed(fn, n):
     return e0.elapsed_time(e1) / G
 
 
-for n in sizes:
-    for _ in range(10):
+import time  # noqa: E402
+t_settle = time.perf_counter()  # settle: clocks ramp up from idle over ~1 s
+while time.perf_counter() - t_settle < 1.5:
+    for n in sizes:
         gate(n)
         stream(n)
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
 res = {k: {n: [] for n in sizes} for k in ("gate", "stream")}
 for r in range(5):
     for n in sizes:

@@ -761,7 +761,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
         const uint32_t pos = (q - blo) * 4 + (uint32_t)L.grp;
         lcrc[pos] = crcs;
         lval[pos] = (uint8_t)(qv >> 31);
-        if (SEAL) write_trailer((uint64_t)q * 4 + (uint64_t)L.grp, crcs);
       }
     };
     if (t > 0) stage((int)t, acc_crc, acc_qv);
@@ -774,6 +773,21 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
     const uint64_t f0 = (uint64_t)blo * 4;
     if (p.crc_out)
       for (uint32_t i = threadIdx.x; i < nfr; i += WAVES * 64) *as_global<g_u32w>(p.crc_out + f0 + i) = lcrc[i];
+    if (SEAL) {  // the workgroup's trailers in frame order, one burst after its reads, non-temporal
+      for (uint32_t i = threadIdx.x; i < nfr; i += WAVES * 64) {
+        const uint32_t v = __builtin_bswap32(lcrc[i]);
+        uint8_t* a = p.wbytes + (f0 + i) * stride + n;
+        if (((uintptr_t)a & 3u) == 0) {
+          __builtin_nontemporal_store(v, as_global<g_u32w>((uint32_t*)a));
+        } else {
+          g_u8w* wp = as_global<g_u8w>(a);
+          __builtin_nontemporal_store((uint8_t)v, wp);
+          __builtin_nontemporal_store((uint8_t)(v >> 8), wp + 1);
+          __builtin_nontemporal_store((uint8_t)(v >> 16), wp + 2);
+          __builtin_nontemporal_store((uint8_t)(v >> 24), wp + 3);
+        }
+      }
+    }
     if (!SEAL && p.valid_out) {
       if ((((uintptr_t)(p.valid_out + f0)) & 3u) == 0) {
         for (uint32_t i = threadIdx.x; i < nfr / 4; i += WAVES * 64)
