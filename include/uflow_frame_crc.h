@@ -106,8 +106,8 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 #define UFC_VARLEN_STREAM 7      /*   (tuning) byte-balanced streams: 8-lane groups walk equal byte ranges (CSR) */
 #define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
 #define UFC_OPT_SEAL_KERNEL 3    /* fixed-stride seals: */
-#define UFC_SEAL_TWO_PASS 0      /*   validate kernel's CRC words, then a non-temporal trailer pass (default) */
-#define UFC_SEAL_INLINE 1        /*   trailers written by the CRC kernel itself (round-1/2 default) */
+#define UFC_SEAL_INLINE 0        /*   the CRC kernel writes each workgroup's trailers after its reads (default) */
+#define UFC_SEAL_TWO_PASS 1      /*   validate kernel's CRC words, then a non-temporal trailer pass (round-3 default) */
 #define UFC_OPT_COUNT_ 4
 int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value);
 int ufc_ctx_get_option(const ufc_ctx* ctx, int option);

@@ -25,6 +25,8 @@ world = int(os.environ["WORLD_SIZE"])
 os.environ["NCCL_HOSTID"] = f"ufc-test-rank{rank}"
 os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
 os.environ.setdefault("NCCL_IB_DISABLE", "1")
+if "--timeout" in sys.argv:
+    os.environ.setdefault("UFC_SHARD_TRACE", "1")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -35,7 +35,7 @@ UFC_OPT_FIXED_KERNEL, UFC_OPT_VARLEN_KERNEL, UFC_OPT_GENERIC_JC = 0, 1, 2
 UFC_FIXED_AUTO, UFC_FIXED_GENERIC, UFC_FIXED_CLAIM16 = 0, 1, 2
 UFC_VARLEN_AUTO, UFC_VARLEN_GENERIC, UFC_VARLEN_SORTED, UFC_VARLEN_BLOCKED8, UFC_VARLEN_CLAIM16 = 0, 1, 2, 3, 4
 UFC_VARLEN_BLOCKSTREAM, UFC_VARLEN_SORTED8, UFC_VARLEN_STREAM = 5, 6, 7
-UFC_OPT_SEAL_KERNEL, UFC_SEAL_TWO_PASS, UFC_SEAL_INLINE = 3, 0, 1
+UFC_OPT_SEAL_KERNEL, UFC_SEAL_INLINE, UFC_SEAL_TWO_PASS = 3, 0, 1
 
 # Every symbol the header declares, with its ctypes signature.
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)

@@ -365,7 +365,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   constexpr bool NO_FINISH = ABL_ == 5;
   constexpr int ABL = NO_FINISH ? kLeanAblLoads : ABL_;
   constexpr bool DYN = SCHED == kSchedClaim;        // claimed sets (per-workgroup counter)
-  constexpr bool ILV = SCHED == kSchedInterleave;   // static: wave i takes lo + i + k * WAVES
+  constexpr bool ILV = SCHED == kSchedInterleave || SCHED == kSchedFine;  // static: wave i takes lo + i + k * WAVES
   constexpr uint32_t kInc = ILV ? (uint32_t)WAVES : 1u;  // step of a static sequence
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
 #ifdef UFC_TUNING
@@ -517,11 +517,9 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       t = 0;
     }
   };
-  // Frame-set processing from a loaded item (J blocks).
-  auto compute = [&](uint32_t q, const ItemBuf<J>& b, Chains& c) {
-#pragma unroll
-    for (int j = 0; j < J; j++) {
-      uint4 x = b.x[j];
+  // Frame-set processing from a loaded item (J blocks), block by block.
+  auto compute_block = [&](uint32_t q, int j, uint4 x, Chains& c) {
+    {
       if (ABL == kLeanAblCompute && j == 0) {  // not loop-invariant
         x.x ^= q; x.y ^= q; x.z ^= q; x.w ^= q;
       }
@@ -548,6 +546,10 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
         c.v3 = chain_step(L.lds, c.v3, L.K, x.w);
       }
     }
+  };
+  auto compute = [&](uint32_t q, const ItemBuf<J>& b, Chains& c) {
+#pragma unroll
+    for (int j = 0; j < J; j++) compute_block(q, j, b.x[j], c);
   };
   // Loads of a main-loop set: a wave-uniform set base (SGPRs) plus this lane's loop-invariant
   // 32-bit offset, so no per-set VGPR address arithmetic (whose registers the allocator may take
@@ -695,6 +697,30 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       finish(q_cur, c, false);
       q_cur += kInc;
       load(q_cur, A);
+    }
+  } else if (SCHED == kSchedFine) {
+    // Interleaved schedule, the next set's loads issued one block at a time between the current
+    // set's blocks, so a wave's bytes in flight stay level instead of arriving in bursts of one set
+    // (tuning A/B).  The compute runs even for a set past the range (its result is not kept).
+    auto step_fine = [&](ItemBuf<J>& cur, ItemBuf<J>& fill) {
+      const uint32_t q_load = q_nx1;
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)set_base(q_load), 0, (int)kFixRecords, kFixRsrcWord3);
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(voff + 256u * j), 0, kFixAuxNT);
+        fill.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+        __builtin_amdgcn_sched_barrier(0);
+        compute_block(q_cur, j, cur.x[j], c);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (q_cur < q_end) finish(q_cur, c, false);
+      q_cur = q_load;
+      q_nx1 = q_load + kInc;
+    };
+    while (q_cur < q_end) {
+      step_fine(A, B);
+      step_fine(B, A);
     }
   } else if (DEPTH == 2 && !DYN) {  // static schedules: no claim ring, rounds of two steps
     while (q_cur < q_end) {
@@ -916,6 +942,8 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
     return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 16>
                     : (const void*)frame_crc_fixed_kernel<6, false, 1, kLeanAblLoads, kSchedInterleave, 16>;
   }
+  if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedFine && abl == 0)
+    return (const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedFine, 8>;
   if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedInterleave && abl == 5)
     return (const void*)frame_crc_fixed_kernel<6, false, 2, 5, kSchedInterleave, 8>;
   if (J == 6 && !seal && (depth == 2 || depth == 3) && abl >= 0 && abl <= 2 && sched >= 0 && sched <= 2) {

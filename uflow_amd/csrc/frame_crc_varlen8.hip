@@ -666,10 +666,12 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, 12, 2, true, 64, kV8Aux, true>(const KernelParams);
 // Product: 12 waves, 2 sets per wave in the ring (three waves per SIMD; config 3 1.69 ms kernel
 // against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill), runs sorted
-// in the kernel.  The pre-sorted variant (records from sort_runs) is kept for A/B in tuning builds.
-UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
+// in the kernel with per-run geometry (GEOR: 1.480 against 1.506 ms, config 3, in-process A/B,
+// identical results).  Per-set geometry and the pre-sorted variant (records from sort_runs) are
+// kept for A/B in tuning builds.
 UFC_V8_INSTG(false, false) UFC_V8_INSTG(true, false) UFC_V8_INSTG(false, true) UFC_V8_INSTG(true, true)
 #ifdef UFC_TUNING
+UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
 UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
 UFC_V8_INSTW(false, 8) UFC_V8_INSTW(false, 16) UFC_V8_INSTW(false, 32) UFC_V8_INSTW(true, 8) UFC_V8_INSTW(true, 16)
 UFC_V8_INSTW(true, 32) UFC_V8_INSTA(8) UFC_V8_INSTA(16) UFC_V8_INSTA(32) UFC_V8_INSTA(64)
@@ -1094,17 +1096,13 @@ const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw,
       default: return nullptr;
     }
   }
-#else
-  if (sortw != 64 || aux != kV8Aux) return nullptr;
-#endif
-  if (insort) {
+  if (insort) {  // per-set geometry (the round-3 product)
     if (pairs)
       return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true>
                   : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, true>;
     return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true>
                 : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true>;
   }
-#ifdef UFC_TUNING
   if (pairs)
     return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, false>
                 : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, false>;

@@ -334,7 +334,7 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
 #endif
   const int waves = 12;
   int sortw = 64, aux = 0;  // runs sorted whole, default-policy loads; UFC_V8_SORTW / UFC_V8_AUX (tuning): A/B
-  bool geor = false;        // per-run geometry (UFC_V8_GEOR, tuning A/B)
+  bool geor = true;         // per-run geometry (product); UFC_V8_GEOR=0 (tuning): per-set geometry
 #ifdef UFC_TUNING
   if (const char* sw = std::getenv("UFC_V8_SORTW")) sortw = std::atoi(sw);
   if (const char* ax = std::getenv("UFC_V8_AUX")) aux = std::atoi(ax);
@@ -539,7 +539,7 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
       if (value != 0 && !ufc_dev::config_available(value)) return UFC_ERR_INVALID_ARG;
       break;
     case UFC_OPT_SEAL_KERNEL:
-      if (value < UFC_SEAL_TWO_PASS || value > UFC_SEAL_INLINE) return UFC_ERR_INVALID_ARG;
+      if (value != UFC_SEAL_INLINE && value != UFC_SEAL_TWO_PASS) return UFC_ERR_INVALID_ARG;
       break;
     default: return UFC_ERR_INVALID_ARG;
   }
@@ -602,7 +602,7 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
                                       : std::strcmp(k, "sorted8") == 0 ? UFC_VARLEN_SORTED8 : UFC_VARLEN_AUTO;
   if (const char* j = std::getenv("UFC_FIXED_JC")) ctx->opt[UFC_OPT_GENERIC_JC] = std::atoi(j);
   if (const char* k = std::getenv("UFC_SEAL_KERNEL"))
-    ctx->opt[UFC_OPT_SEAL_KERNEL] = std::strcmp(k, "inline") == 0 ? UFC_SEAL_INLINE : UFC_SEAL_TWO_PASS;
+    ctx->opt[UFC_OPT_SEAL_KERNEL] = std::strcmp(k, "two_pass") == 0 ? UFC_SEAL_TWO_PASS : UFC_SEAL_INLINE;
 #endif
   *out = ctx;
   return UFC_OK;
@@ -744,11 +744,12 @@ int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t 
   kp.crc_out = d_crc_out;
   DeviceGuard g(ctx->device);
   if (const int lean = lean_fixed_blocks(ctx, frame_len, stride, n)) {
-    if (ctx->opt[UFC_OPT_SEAL_KERNEL] == UFC_SEAL_INLINE)  // A/B: trailers written by the CRC kernel
-      return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
-    // Two passes: the validate kernel's CRC words (into the caller's
-    // crc_out, or per-stream scratch), then every trailer with non-temporal stores once the whole
-    // batch has been read.
+    // Default: the CRC kernel writes its trailers itself, each workgroup after its last read, in
+    // frame order from the LDS-staged results with non-temporal stores (DESIGN.md section 5.3:
+    // 0.2665 against 0.2795 ms for two passes, config 2's 1M x 1500 B).
+    if (ctx->opt[UFC_OPT_SEAL_KERNEL] == UFC_SEAL_INLINE) return launch_lean_fixed(ctx, lean, true, kp, (hipStream_t)stream);
+    // UFC_SEAL_TWO_PASS: the validate kernel's CRC words (into the caller's crc_out, or per-stream
+    // scratch), then every trailer with non-temporal stores once the whole batch has been read.
     uint32_t* crc = d_crc_out;
     hipError_t e;
     if (!crc && (e = stream_scratch(ctx, kScratchSealCrc, (hipStream_t)stream, n * 4, (void**)&crc)) != hipSuccess)

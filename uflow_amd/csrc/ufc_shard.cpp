@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -185,9 +186,28 @@ int abort_comm(ufc_comm* comm, int rc) {
 // (a missing shard pointer) then fails the call on every rank -- UFC_ERR_PEER on the others -- and
 // the communicator stays usable.  The wait polls with a deadline (timeout_ms): a peer that never
 // makes the call (crashed, or calling something else) aborts both communicators instead of hanging.
+// UFC_SHARD_TRACE=1: progress of the status agreement on stderr (diagnosing a peer that never joins).
+bool shard_trace() {
+  static const bool on = [] {
+    const char* t = std::getenv("UFC_SHARD_TRACE");
+    return t && *t && *t != '0';
+  }();
+  return on;
+}
+#define UFC_TRACE(...)                                        \
+  do {                                                        \
+    if (shard_trace()) {                                      \
+      std::fprintf(stderr, "[ufc_shard rank %d] ", comm->rank); \
+      std::fprintf(stderr, __VA_ARGS__);                      \
+      std::fprintf(stderr, "\n");                             \
+      std::fflush(stderr);                                    \
+    }                                                         \
+  } while (0)
+
 int agree_status(ufc_comm* comm, int local_rc) {
   if (comm->nranks == 1) return local_rc;
   const Rccl& r = rccl();
+  UFC_TRACE("agree_status: local %d, enqueueing", local_rc);
   comm->h_status[0] = local_rc != UFC_OK ? 1 : 0;
   comm->h_status[1] = -1;
   hipError_t e = hipMemcpyAsync(comm->d_status, comm->h_status, 4, hipMemcpyHostToDevice, comm->ctl_stream);
@@ -198,6 +218,7 @@ int agree_status(ufc_comm* comm, int local_rc) {
   const ncclResult_t nr = r.AllReduce(comm->d_status, comm->d_status, 1, ncclInt32, ncclMax, comm->ctl,
                                       comm->ctl_stream);
   if (nr != ncclSuccess) return abort_comm(comm, nccl_fail(comm, nr));
+  UFC_TRACE("agree_status: all-reduce enqueued");
   if ((e = hipMemcpyAsync(comm->h_status + 1, comm->d_status, 4, hipMemcpyDeviceToHost, comm->ctl_stream)) !=
       hipSuccess) {
     ufc_internal::note_hip_error(comm->ctx, (int)e);
@@ -215,10 +236,15 @@ int agree_status(ufc_comm* comm, int local_rc) {
     if (r.CommGetAsyncError(comm->ctl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
       return abort_comm(comm, nccl_fail(comm, ae));
     const auto waited = std::chrono::steady_clock::now() - t0;
-    if (comm->timeout_ms > 0 && waited > std::chrono::milliseconds(comm->timeout_ms))
-      return abort_comm(comm, UFC_ERR_TIMEOUT);
+    if (comm->timeout_ms > 0 && waited > std::chrono::milliseconds(comm->timeout_ms)) {
+      UFC_TRACE("agree_status: deadline passed, aborting");
+      const int rc = abort_comm(comm, UFC_ERR_TIMEOUT);
+      UFC_TRACE("agree_status: aborted");
+      return rc;
+    }
     if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(spin > 20000 ? 1000 : 20));
   }
+  UFC_TRACE("agree_status: agreed %d", comm->h_status[1]);
   if (local_rc != UFC_OK) return local_rc;
   return comm->h_status[1] != 0 ? UFC_ERR_PEER : UFC_OK;
 }
