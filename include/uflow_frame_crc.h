@@ -58,7 +58,6 @@ extern "C" {
 #define UFC_ERR_NOMEM (-4)
 #define UFC_ERR_COMM (-5) /* RCCL missing or failed (multi-GPU entry points; see ufc_comm_last_error) */
 #define UFC_ERR_PEER (-6) /* multi-GPU: another rank rejected its part of this call; nothing was transferred */
-#define UFC_ERR_TIMEOUT (-7) /* multi-GPU: the peers did not join the call's status agreement in time */
 
 /* Frame constants from the reference (src/frame/serial/mod.rs:11-13, src/lib.rs:286-294). */
 #define UFC_FRAME_CRC_SIZE 4
@@ -218,9 +217,6 @@ int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const ui
 int ufc_comm_destroy(ufc_comm* comm);
 /* Last RCCL result code seen by this communicator (0 if none). */
 int ufc_comm_last_error(const ufc_comm* comm);
-/* How long a sharded call waits for the peers to join its status agreement (below) before it aborts
- * the communicator and returns UFC_ERR_TIMEOUT; 0 = forever.  Default 300000 ms. */
-int ufc_comm_set_timeout(ufc_comm* comm, int timeout_ms);
 /* Collective: the batched gate on this rank's shard, then the gather to `root`.
  *   d_frames     this rank's shard (frame k of the shard at d_frames + k * stride, stride >= frame_len)
  *   d_crc_out    root: n_total words in global frame order; other ranks: their shard's words
@@ -235,9 +231,10 @@ int ufc_comm_set_timeout(ufc_comm* comm, int timeout_ms);
  * rank sees alike are checked before any transfer, so a bad call fails on every rank.  Arguments
  * only this rank can check (its shard pointers) are agreed before any transfer with a one-word
  * all-reduce on a second communicator: a rank that rejects its part returns UFC_ERR_INVALID_ARG,
- * every other rank UFC_ERR_PEER, nothing is queued and the communicator stays usable.  That wait has
- * a deadline (ufc_comm_set_timeout): a peer that never joins aborts the communicator
- * (UFC_ERR_TIMEOUT).  A failure that only this rank sees after the gather has begun (a HIP launch
+ * every other rank UFC_ERR_PEER, nothing is queued and the communicator stays usable.  Like any RCCL
+ * collective, the call waits for every peer to make it: a peer that never does (crashed, or calling
+ * something else) is the caller's job supervision to detect (there is no deadline: ncclCommAbort
+ * measured not to return while the peer has not joined, on the socket transport).  A failure that only this rank sees after the gather has begun (a HIP launch
  * error) aborts the communicator (ncclCommAbort) and marks it unusable (later calls return
  * UFC_ERR_COMM): the peers' transfers then fail or stall, and the caller must tear down every
  * rank's communicator. */

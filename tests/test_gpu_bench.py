@@ -39,7 +39,9 @@ def test_bench_sharded_path_one_rank():
     j = _run(["--sharded", "--global-frames", "5000000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline",
               "--settle-ms", "5"])
     assert j["scaling"] == "strong" and j["config"]["global_frames"] == 5_000_000
-    assert "bit-exact vs the oracle: True" in j["data"] and "valid flags as planted: True" in j["data"]
+    assert "CRC words gathered on rank 0 == the CPU oracle over every rank's shard: True" in j["data"]
+    assert "oracle valid flags == planted flips on every rank: True" in j["data"]
+    assert "valid flags as planted: True" in j["data"]
     assert "ufc_crc_sharded" in j["roofline"]["kernel"]
 
 
@@ -50,5 +52,7 @@ def test_bench_two_ranks_one_device():
     j = _run(["--gpus", "2", "--one-device", "--global-frames", "10000000", "--steps", "3", "--warmup", "1",
               "--settle-ms", "5", "--cpu-seconds", "0.5"], timeout=300)
     assert j["n_gpus"] == 2 and j["scaling"] == "strong" and j["config"]["global_frames"] == 10_000_000
-    assert "bit-exact vs the oracle: True" in j["data"] and "valid flags as planted: True" in j["data"]
+    assert "all 10000000 CRC words gathered on rank 0 == the CPU oracle over every rank's shard: True" in j["data"]
+    assert "oracle valid flags == planted flips on every rank: True" in j["data"]
+    assert "valid flags as planted: True" in j["data"]
     assert j["cpu_baseline"]["value"] > 0 and j["roofline"]["ceiling_GBs"] > 0

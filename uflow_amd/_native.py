@@ -25,7 +25,6 @@ UFC_ERR_HIP = -3
 UFC_ERR_NOMEM = -4
 UFC_ERR_COMM = -5
 UFC_ERR_PEER = -6
-UFC_ERR_TIMEOUT = -7
 UFC_COMM_ID_BYTES = 128
 UFC_MAX_RANKS = 64
 UFC_OP_GATE, UFC_OP_SEND, UFC_OP_RECV = 0, 1, 2
@@ -88,7 +87,6 @@ _SIGNATURES = {
                                        ctypes.c_void_p]),
     "ufc_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "ufc_comm_last_error": (ctypes.c_int, [ctypes.c_void_p]),
-    "ufc_comm_set_timeout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ufc_crc_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "ufc_crc_sharded_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

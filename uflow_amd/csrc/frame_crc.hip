@@ -357,7 +357,11 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 // workgroup to finish resets both, so every launch finds them zero (launches of one slot are
 // stream-ordered; see ufc_api.cpp).
 
-template <int J, bool SEAL, int DEPTH, int ABL_, int SCHED, int WAVES>
+// LOADV (tuning A/B of the main loop's loads): bit 0 = pieces of block 0 wholly before G load
+// nothing (an out-of-range offset: zeros, no memory request; the front fix zeroes them anyway);
+// bit 1 = default cache policy for the first and last block (the lines a frame shares with its
+// neighbours) and non-temporal for the rest.
+template <int J, bool SEAL, int DEPTH, int ABL_, int SCHED, int WAVES, int LOADV = 0>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const KernelParams p) {
   static_assert(DEPTH >= 1 && DEPTH <= 3, "pipeline depth (4 spills at J = 6)");
   static_assert(DEPTH != 1 || SCHED != kSchedClaim, "depth 1: static schedules only");
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   constexpr bool NO_FINISH = ABL_ == 5;
   constexpr int ABL = NO_FINISH ? kLeanAblLoads : ABL_;
   constexpr bool DYN = SCHED == kSchedClaim;        // claimed sets (per-workgroup counter)
-  constexpr bool ILV = SCHED == kSchedInterleave || SCHED == kSchedFine;  // static: wave i takes lo + i + k * WAVES
+  constexpr bool ILV = SCHED == kSchedInterleave;   // static: wave i takes lo + i + k * WAVES
   constexpr uint32_t kInc = ILV ? (uint32_t)WAVES : 1u;  // step of a static sequence
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
 #ifdef UFC_TUNING
@@ -587,7 +591,26 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       b.x[j] = v;
     }
   };
-  auto load = [&](uint32_t q, ItemBuf<J>& b) { load_set<J>(set_base(q), voff, b); };
+  // LOADV bit 0: this lane's block-0 offset (out of range for a piece wholly before G)
+  const uint32_t voff_b0 = ((LOADV & 1) && 16 * L.col + 16 <= pad - 4) ? kFixRecords : voff;
+  auto load = [&](uint32_t q, ItemBuf<J>& b) {
+    if constexpr (LOADV == 0) {
+      load_set<J>(set_base(q), voff, b);
+    } else {
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)set_base(q), 0, (int)kFixRecords, kFixRsrcWord3);
+#pragma unroll
+      for (int j = 0; j < J; j++) {
+        const uint32_t o = (j == 0 ? voff_b0 : voff) + 256u * j;
+        u32x4 v;
+        if ((LOADV & 2) && (j == 0 || j == J - 1))
+          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0);
+        else
+          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, kFixAuxNT);
+        b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
+      }
+    }
+  };
   // The partial last set: lanes of frames past nframes re-read frame nframes - 1.
   auto load_tail = [&](ItemBuf<J>& b) {
     const int64_t room = (int64_t)(p.nframes - 1 - 4 * (uint64_t)nfull);
@@ -697,30 +720,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       finish(q_cur, c, false);
       q_cur += kInc;
       load(q_cur, A);
-    }
-  } else if (SCHED == kSchedFine) {
-    // Interleaved schedule, the next set's loads issued one block at a time between the current
-    // set's blocks, so a wave's bytes in flight stay level instead of arriving in bursts of one set
-    // (tuning A/B).  The compute runs even for a set past the range (its result is not kept).
-    auto step_fine = [&](ItemBuf<J>& cur, ItemBuf<J>& fill) {
-      const uint32_t q_load = q_nx1;
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)set_base(q_load), 0, (int)kFixRecords, kFixRsrcWord3);
-#pragma unroll
-      for (int j = 0; j < J; j++) {
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(voff + 256u * j), 0, kFixAuxNT);
-        fill.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-        __builtin_amdgcn_sched_barrier(0);
-        compute_block(q_cur, j, cur.x[j], c);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (q_cur < q_end) finish(q_cur, c, false);
-      q_cur = q_load;
-      q_nx1 = q_load + kInc;
-    };
-    while (q_cur < q_end) {
-      step_fine(A, B);
-      step_fine(B, A);
     }
   } else if (DEPTH == 2 && !DYN) {  // static schedules: no claim ring, rounds of two steps
     while (q_cur < q_end) {
@@ -942,8 +941,16 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
     return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 16>
                     : (const void*)frame_crc_fixed_kernel<6, false, 1, kLeanAblLoads, kSchedInterleave, 16>;
   }
-  if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedFine && abl == 0)
-    return (const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedFine, 8>;
+  if (J == 6 && depth == 2 && waves == 8 && sched == kSchedInterleave && abl >= 10 && abl <= 12) {  // LOADV 1..3
+    static const void* const lv[3][2] = {
+        {(const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, 1>,
+         (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, 1>},
+        {(const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, 2>,
+         (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, 2>},
+        {(const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, 3>,
+         (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, 3>}};
+    return lv[abl - 10][seal ? 1 : 0];
+  }
   if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedInterleave && abl == 5)
     return (const void*)frame_crc_fixed_kernel<6, false, 2, 5, kSchedInterleave, 8>;
   if (J == 6 && !seal && (depth == 2 || depth == 3) && abl >= 0 && abl <= 2 && sched >= 0 && sched <= 2) {

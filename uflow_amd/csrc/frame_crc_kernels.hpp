@@ -53,7 +53,6 @@ constexpr int kSchedRange = 0;
 constexpr int kSchedClaim = 1;
 constexpr int kSchedInterleave = 2;
 constexpr int kSchedBlocked = 3;  // static: runs of 16 consecutive sets, interleaved over the waves
-constexpr int kSchedFine = 4;     // interleaved, next set's loads issued block by block (tuning A/B)
 constexpr int kLeanSchedDefault = kSchedInterleave;
 const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves);
 // Lean variable-length kernel (CSR offsets, any frame lengths; frames of 4..1532 B on the fast

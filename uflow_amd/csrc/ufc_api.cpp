@@ -167,6 +167,8 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
 #endif
 #ifdef UFC_TUNING
   if (const char* wv = std::getenv("UFC_LEAN_WAVES")) waves = std::atoi(wv);  // A/B: 8 or 16
+  if (const char* lv = std::getenv("UFC_LEAN_LOADV"))  // A/B of the main loop's loads (LOADV 1..3)
+    if (std::atoi(lv) >= 1 && std::atoi(lv) <= 3) abl = 9 + std::atoi(lv);
 #endif
   const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl, sched, waves);
   if (!fn) return UFC_ERR_INVALID_ARG;
@@ -512,7 +514,6 @@ const char* ufc_error_string(int code) {
     case UFC_ERR_NOMEM: return "out of memory";
     case UFC_ERR_COMM: return "RCCL unavailable or failed (see ufc_comm_last_error)";
     case UFC_ERR_PEER: return "another rank rejected its part of this sharded call (nothing was transferred)";
-    case UFC_ERR_TIMEOUT: return "the peer ranks did not join the sharded call in time (communicator aborted)";
     default: return "unknown error";
   }
 }

@@ -106,7 +106,6 @@ struct ufc_comm {
   hipStream_t ctl_stream = nullptr;
   int32_t* d_status = nullptr;
   int32_t* h_status = nullptr;  // [0] this rank's status, [1] the agreed (max over ranks)
-  int timeout_ms = 300000;
   int last_nccl_error = 0;
   bool broken = false;  // aborted after a rank-local failure mid-gather: every later call fails
   hipEvent_t ev[kMaxChunks] = {};
@@ -184,8 +183,9 @@ int abort_comm(ufc_comm* comm, int rc) {
 // Every rank's verdict on its own arguments, agreed before any transfer is queued: a one-word
 // max-all-reduce on the control communicator, read back through pinned memory.  A rank-local failure
 // (a missing shard pointer) then fails the call on every rank -- UFC_ERR_PEER on the others -- and
-// the communicator stays usable.  The wait polls with a deadline (timeout_ms): a peer that never
-// makes the call (crashed, or calling something else) aborts both communicators instead of hanging.
+// the communicator stays usable.  The wait polls the stream and the control communicator's
+// asynchronous error (a peer that never makes the call is left to the caller's supervision: RCCL's
+// abort measured not to return while that peer's side of the all-reduce is missing).
 // UFC_SHARD_TRACE=1: progress of the status agreement on stderr (diagnosing a peer that never joins).
 bool shard_trace() {
   static const bool on = [] {
@@ -224,7 +224,6 @@ int agree_status(ufc_comm* comm, int local_rc) {
     ufc_internal::note_hip_error(comm->ctx, (int)e);
     return abort_comm(comm, UFC_ERR_HIP);
   }
-  const auto t0 = std::chrono::steady_clock::now();
   for (int spin = 0;; spin++) {
     e = hipStreamQuery(comm->ctl_stream);
     if (e == hipSuccess) break;
@@ -235,13 +234,6 @@ int agree_status(ufc_comm* comm, int local_rc) {
     ncclResult_t ae = ncclSuccess;
     if (r.CommGetAsyncError(comm->ctl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
       return abort_comm(comm, nccl_fail(comm, ae));
-    const auto waited = std::chrono::steady_clock::now() - t0;
-    if (comm->timeout_ms > 0 && waited > std::chrono::milliseconds(comm->timeout_ms)) {
-      UFC_TRACE("agree_status: deadline passed, aborting");
-      const int rc = abort_comm(comm, UFC_ERR_TIMEOUT);
-      UFC_TRACE("agree_status: aborted");
-      return rc;
-    }
     if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(spin > 20000 ? 1000 : 20));
   }
   UFC_TRACE("agree_status: agreed %d", comm->h_status[1]);
@@ -452,9 +444,8 @@ int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const ui
     return UFC_ERR_COMM;
   }
   // Connect the control communicator now, while every rank is here: RCCL sets a communicator's
-  // connections up at its first collective, inside the enqueueing call and blocking the host until
-  // the peers join.  Left to the first agree_status, a rank calling alone would block there, before
-  // its deadline is ever checked; connected, the all-reduce only enqueues and the deadline applies.
+  // connections up at its first collective, inside the enqueueing call (blocking the host until the
+  // peers join), so the first sharded call would otherwise pay for it.
   if (nranks > 1) {
     c->h_status[0] = 0;
     he = hipMemcpyAsync(c->d_status, c->h_status, 4, hipMemcpyHostToDevice, c->ctl_stream);
@@ -494,11 +485,6 @@ int ufc_comm_destroy(ufc_comm* comm) {
 
 int ufc_comm_last_error(const ufc_comm* comm) { return comm ? comm->last_nccl_error : 0; }
 
-int ufc_comm_set_timeout(ufc_comm* comm, int timeout_ms) {
-  if (!comm || timeout_ms < 0) return UFC_ERR_INVALID_ARG;
-  comm->timeout_ms = timeout_ms;
-  return UFC_OK;
-}
 
 int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size_t frame_len, uint64_t n_total,
                     uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream) {

@@ -114,9 +114,6 @@ class ShardedGate:
         except Exception:
             pass
 
-    def set_timeout(self, timeout_ms):
-        """ufc_comm_set_timeout: how long a call waits for the peers to join its status agreement."""
-        check(lib().ufc_comm_set_timeout(self._comm, int(timeout_ms)), "ufc_comm_set_timeout")
 
     def local_range(self, n_total):
         return shard_range(n_total, self.rank, self.world)
