@@ -357,11 +357,16 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 // workgroup to finish resets both, so every launch finds them zero (launches of one slot are
 // stream-ordered; see ufc_api.cpp).
 
-// LOADV (tuning A/B of the main loop's loads): bit 0 = pieces of block 0 wholly before G load
-// nothing (an out-of-range offset: zeros, no memory request; the front fix zeroes them anyway);
-// bit 1 = default cache policy for the first and last block (the lines a frame shares with its
-// neighbours) and non-temporal for the rest.
-template <int J, bool SEAL, int DEPTH, int ABL_, int SCHED, int WAVES, int LOADV = 0>
+// LOADV: the main loop's loads, lean_loadv(skip, first, mid, last): `first` / `mid` / `last` = the
+// cache-policy bits (buffer-load aux) of block 0, blocks 1..J-2 and block J-1; skip = pieces of block
+// 0 wholly before G load nothing (an out-of-range offset: zeros, no memory request; the front fix
+// zeroes them anyway).  The lines a frame shares with its neighbours sit in its first and last block.
+constexpr int lean_loadv(int skip, int first, int mid, int last) { return skip | first << 1 | mid << 6 | last << 11; }
+constexpr int kLoadvAllNT = lean_loadv(0, kFixAuxNT, kFixAuxNT, kFixAuxNT);  // rounds 1-3
+// Product (round 4): default policy for block 0, non-temporal for the rest: 0.2277-0.2289 against
+// 0.2372-0.2383 ms per 1M x 1500 B (in-process A/B, identical results; profiles/EXPERIMENTS.md).
+constexpr int kLoadvProduct = lean_loadv(0, 0, kFixAuxNT, kFixAuxNT);
+template <int J, bool SEAL, int DEPTH, int ABL_, int SCHED, int WAVES, int LOADV = kLoadvProduct>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const KernelParams p) {
   static_assert(DEPTH >= 1 && DEPTH <= 3, "pipeline depth (4 spills at J = 6)");
   static_assert(DEPTH != 1 || SCHED != kSchedClaim, "depth 1: static schedules only");
@@ -591,24 +596,23 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       b.x[j] = v;
     }
   };
-  // LOADV bit 0: this lane's block-0 offset (out of range for a piece wholly before G)
+  // lean_loadv skip: this lane's block-0 offset (out of range for a piece wholly before G)
   const uint32_t voff_b0 = ((LOADV & 1) && 16 * L.col + 16 <= pad - 4) ? kFixRecords : voff;
   auto load = [&](uint32_t q, ItemBuf<J>& b) {
-    if constexpr (LOADV == 0) {
-      load_set<J>(set_base(q), voff, b);
-    } else {
-      const __amdgpu_buffer_rsrc_t rs =
-          __builtin_amdgcn_make_buffer_rsrc((void*)set_base(q), 0, (int)kFixRecords, kFixRsrcWord3);
+    constexpr int kAuxFirst = (LOADV >> 1) & 31, kAuxMid = (LOADV >> 6) & 31, kAuxLast = (LOADV >> 11) & 31;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)set_base(q), 0, (int)kFixRecords, kFixRsrcWord3);
 #pragma unroll
-      for (int j = 0; j < J; j++) {
-        const uint32_t o = (j == 0 ? voff_b0 : voff) + 256u * j;
-        u32x4 v;
-        if ((LOADV & 2) && (j == 0 || j == J - 1))
-          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, 0);
-        else
-          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, kFixAuxNT);
-        b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-      }
+    for (int j = 0; j < J; j++) {
+      const uint32_t o = (j == 0 ? voff_b0 : voff) + 256u * j;
+      u32x4 v;
+      if (j == 0)
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, kAuxFirst);
+      else if (j == J - 1)
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, kAuxLast);
+      else
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)o, 0, kAuxMid);
+      b.x[j] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
   // The partial last set: lanes of frames past nframes re-read frame nframes - 1.
@@ -859,7 +863,9 @@ UFC_INST_FIXED(1) UFC_INST_FIXED(2) UFC_INST_FIXED(3) UFC_INST_FIXED(4) UFC_INST
 // lane->address pattern (4 frames per wave-instruction, 256-B runs right-aligned to the frame end),
 // static interleaved schedule, NBUF sets in flight per wave, no LDS (STAGE: the lean kernel's LDS
 // table staging first).  Results are meaningless (an XOR fold per lane lands in crc_out).
-template <int NBUF, int WAVES, bool STAGE>
+// ALIGN (bytes, 0 = none): each frame's window start rounded down to ALIGN (the same J x 256 bytes
+// read per frame), to measure what unaligned 256-byte pieces cost the memory pipeline.
+template <int NBUF, int WAVES, bool STAGE, int ALIGN = 0>
 __global__ __launch_bounds__(WAVES * 64) void fixed_probe_kernel(const KernelParams p) {
   __shared__ __attribute__((aligned(16))) char lds[STAGE ? kLdsBytes : 16];
   constexpr int NI = 6;
@@ -878,7 +884,9 @@ __global__ __launch_bounds__(WAVES * 64) void fixed_probe_kernel(const KernelPar
   auto load = [&](int q, uint4 (&x)[NI]) {
     const int qc = min(q, nsets - 1);
     const int f = lane >> 4, col = lane & 15;
-    int64_t off = (int64_t)qc * 4 * stride + f * stride + 16 * col - (NI * 256 - (int64_t)p.frame_len);
+    int64_t w0 = (int64_t)qc * 4 * stride + f * stride - (NI * 256 - (int64_t)p.frame_len);
+    if (ALIGN) w0 = w0 & ~(int64_t)(ALIGN - 1);
+    int64_t off = w0 + 16 * col;
     off = off < 0 ? 0 : off;
 #pragma unroll
     for (int j = 0; j < NI; j++) {
@@ -934,6 +942,10 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
          {(const void*)fixed_probe_kernel<2, 16, true>, (const void*)fixed_probe_kernel<3, 16, true>}}};
     return ptab[waves == 16][abl == 4][depth - 2];
   }
+  if (J == 6 && !seal && abl >= 6 && abl <= 8)  // loads-only probe, staged tables, 2 sets: aligned windows
+    return abl == 6 ? (const void*)fixed_probe_kernel<2, 8, true, 64>
+                    : abl == 7 ? (const void*)fixed_probe_kernel<2, 8, true, 128>
+                               : (const void*)fixed_probe_kernel<2, 8, true, 256>;
   if (J == 6 && !seal && depth == 1 && sched == kSchedInterleave && (abl == 0 || abl == 1)) {
     if (waves == 8)
       return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 8>
@@ -941,15 +953,19 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
     return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 16>
                     : (const void*)frame_crc_fixed_kernel<6, false, 1, kLeanAblLoads, kSchedInterleave, 16>;
   }
-  if (J == 6 && depth == 2 && waves == 8 && sched == kSchedInterleave && abl >= 10 && abl <= 12) {  // LOADV 1..3
-    static const void* const lv[3][2] = {
-        {(const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, 1>,
-         (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, 1>},
-        {(const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, 2>,
-         (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, 2>},
-        {(const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, 3>,
-         (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, 3>}};
-    return lv[abl - 10][seal ? 1 : 0];
+  if (J == 6 && depth == 2 && waves == 8 && sched == kSchedInterleave && abl >= 100000) {  // LOADV = abl - 100000
+    switch (abl - 100000) {
+#define UFC_LV(V)                                                                          \
+  case V:                                                                                  \
+    return seal ? (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, V> \
+                : (const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, V>;
+      UFC_LV(kLoadvAllNT) UFC_LV(lean_loadv(0, 0, 2, 0)) UFC_LV(lean_loadv(0, 2, 2, 0))
+      UFC_LV(lean_loadv(0, 0, 18, 18)) UFC_LV(lean_loadv(0, 0, 3, 3)) UFC_LV(lean_loadv(0, 1, 2, 2))
+      UFC_LV(lean_loadv(0, 16, 2, 2)) UFC_LV(lean_loadv(1, 0, 2, 2)) UFC_LV(lean_loadv(0, 0, 18, 2))
+      UFC_LV(lean_loadv(0, 0, 2, 18)) UFC_LV(lean_loadv(0, 0, 0, 2))
+#undef UFC_LV
+      default: return nullptr;
+    }
   }
   if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedInterleave && abl == 5)
     return (const void*)frame_crc_fixed_kernel<6, false, 2, 5, kSchedInterleave, 8>;

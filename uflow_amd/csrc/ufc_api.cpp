@@ -167,8 +167,11 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
 #endif
 #ifdef UFC_TUNING
   if (const char* wv = std::getenv("UFC_LEAN_WAVES")) waves = std::atoi(wv);  // A/B: 8 or 16
-  if (const char* lv = std::getenv("UFC_LEAN_LOADV"))  // A/B of the main loop's loads (LOADV 1..3)
-    if (std::atoi(lv) >= 1 && std::atoi(lv) <= 3) abl = 9 + std::atoi(lv);
+  // A/B of the main loop's loads: UFC_LEAN_LOADV=skip:first:mid:last (frame_crc.hip lean_loadv)
+  if (const char* lv = std::getenv("UFC_LEAN_LOADV")) {
+    int sk = 0, f = 0, m = 0, l = 0;
+    if (std::sscanf(lv, "%d:%d:%d:%d", &sk, &f, &m, &l) == 4) abl = 100000 + (sk | f << 1 | m << 6 | l << 11);
+  }
 #endif
   const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl, sched, waves);
   if (!fn) return UFC_ERR_INVALID_ARG;
