@@ -28,8 +28,11 @@ WORKLOADS = {
     "varlen": [("config 3 validate", "frame_crc_varlen8_kernel<false, false", "varlen")],
     "shard": [("config 4 per-GPU shard validate (3 launches of 4.17M frames)", "frame_crc_fixed_kernel<6, false",
                SHARD // 3 * (L2 + 5))],
-    "seal": [("config 2 seal, pass 1 (CRC words)", "frame_crc_fixed_kernel<6, false", N2 * (L2 + 4)),
-             ("config 2 seal, pass 2 (trailer stores)", "seal_scatter_kernel", N2 * 8)],
+    "seal": [("config 2 seal, one kernel (product: each workgroup's trailers after its reads)",
+              "frame_crc_fixed_kernel<6, true", N2 * (L2 + 4)),
+             ("config 2 seal, two passes (comparison): pass 1 (CRC words)", "frame_crc_fixed_kernel<6, false",
+              N2 * (L2 + 4)),
+             ("config 2 seal, two passes (comparison): pass 2 (trailer stores)", "seal_scatter_kernel", N2 * 8)],
     "seal_varlen": [("config 3 seal", "frame_crc_varlen8_kernel<true, false", "seal_varlen")],
     "parse": [("parse walk", "parse_walk", None), ("parse emit", "parse_emit", None)],
 }

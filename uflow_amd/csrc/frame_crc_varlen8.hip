@@ -30,6 +30,8 @@
 //     longer than 6 blocks, at the batch edges, past its end) run byte-wise, in the same loop.
 #include "frame_crc_dev.hpp"
 
+#include <cstdlib>
+
 namespace ufc_dev {
 
 namespace {
@@ -129,7 +131,7 @@ __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
 // FREEZE: chains stop after the frame's own J blocks.
 template <bool FREEZE>
 __device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, uint32_t pad, uint32_t t, bool g1,
-                                       bool last_any, uint4 x0, uint4 x1, Chains& c) {
+                                       bool last_any, uint4 x0, uint4 x1, Chains& c, bool skip0 = false) {
   if (FREEZE ? (j + 1 == J) : last_any) {
     c.tr = t ? __builtin_amdgcn_alignbyte(x1.w, x1.z, 4u - t) : x1.w;
     if (L.col == 7u) {  // the trailer and the bytes past the frame are CRC'd as zeros
@@ -138,8 +140,15 @@ __device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, u
     }
   }
   if (j == 0) {
-    const uint4 f0 = fix_piece(L.lds, x0, (int)pad - (int)(16u * L.col));
     x1 = fix_piece(L.lds, x1, (int)pad - 128 - (int)(16u * L.col));
+    if (skip0) {  // (wave-uniform) A^128(0) ^ x1 = x1: no chain step on the zero first piece
+      c.v0 = x1.x;
+      c.v1 = x1.y;
+      c.v2 = x1.z;
+      c.v3 = x1.w;
+      return;
+    }
+    const uint4 f0 = fix_piece(L.lds, x0, (int)pad - (int)(16u * L.col));
     c.v0 = f0.x;
     c.v1 = f0.y;
     c.v2 = f0.z;
@@ -170,6 +179,7 @@ struct Set8Meta {
   bool slow;      // byte path
   bool mixed;     // block counts differ
   bool g1;        // a frame's G straddles into block 1 (pad > 256)
+  bool skip0;     // (PSORT) every frame's first piece is zeros: the chains start at the second piece
 };
 
 template <int J>
@@ -190,7 +200,11 @@ struct Buf8 {
 // half-row DPP reductions and ballots; a set then takes its two words per group with ds_bpermute
 // and its set-level bits with one readfirstlane.  Frames the fast path cannot take sort together
 // (key 7), so they spoil fewer sets.
-template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux, bool GEOR = false>
+// PSORT (with GEOR): runs sorted by 128-byte piece count P instead of block count J (sets then share
+// P as well as J), and a set whose frames all have >= 132 pad bytes -- its first piece is zeros in
+// every lane -- starts its chains at the second piece (no chain step on a zero state).
+template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux, bool GEOR = false,
+          bool PSORT = false>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
   static_assert(SORTW == 8 || SORTW == 16 || SORTW == 32 || SORTW == 64, "sort window");
   static_assert(!GEOR || INSORT, "per-run geometry needs the in-kernel sort");
@@ -280,6 +294,10 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       sb = run_base(a);
       fg = frame_geo(a, len, live, sb);
       key = !live ? 8u : (fg.bad ? 7u : (uint32_t)J);
+      if constexpr (PSORT) {  // P = ceil((len + t + 4) / 128) = 2J or 2J - 1 (pad >= 128)
+        const uint32_t P = 2u * ((fg.geo >> 9) & 7u) - ((fg.geo & 511u) >= 128u ? 1u : 0u);
+        key = !live ? 14u : (fg.bad ? 13u : P);
+      }
     }
     if constexpr (SORTW == 8) {  // sets of consecutive frames: no reordering
       out.a_lo = (uint32_t)a;
@@ -290,8 +308,9 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     }
     const uint64_t qmask = SORTW == 64 ? ~0ull : (((1ull << SORTW) - 1ull) << (L.lane & ~(uint32_t)(SORTW - 1)));
     uint32_t below = 0, rank_in = 0;
+    constexpr uint32_t kMaxKey = PSORT ? 14u : 8u;
 #pragma unroll
-    for (uint32_t k = 1; k <= 8; k++) {
+    for (uint32_t k = 1; k <= kMaxKey; k++) {
       const uint64_t m = __builtin_amdgcn_ballot_w64(key == k) & qmask;
       below += (k < key) ? (uint32_t)__builtin_popcountll(m) : 0u;
       const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -317,7 +336,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
         const uint64_t mg1 = __builtin_amdgcn_ballot_w64((geo & 511u) > 256u);
         const uint32_t s8 = L.lane & ~7u;
         const uint32_t slow = ((mbad >> s8) & 0xFFu) != 0 ? 1u : 0u, g1 = ((mg1 >> s8) & 0xFFu) != 0 ? 1u : 0u;
-        out.a_lo = geo | (min(jx, (uint32_t)JM) << 24) | ((jx != jn ? 1u : 0u) << 27) | (slow << 28) | (g1 << 29);
+        uint32_t skip0 = 0;
+        if constexpr (PSORT) {  // every frame of the set: >= 132 pad bytes (piece 0 all zeros, G in piece 1)
+          const uint64_t mz = __builtin_amdgcn_ballot_w64((geo & 511u) >= 132u);
+          skip0 = ((mz >> s8) & 0xFFu) == 0xFFu ? 1u : 0u;
+        }
+        out.a_lo = geo | (min(jx, (uint32_t)JM) << 24) | ((jx != jn ? 1u : 0u) << 27) | (slow << 28) | (g1 << 29) |
+                   (skip0 << 30);
         return;
       }
     }
@@ -392,6 +417,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       m.mixed = ((gu >> 27) & 1u) != 0;
       m.slow = ((gu >> 28) & 1u) != 0;
       m.g1 = ((gu >> 29) & 1u) != 0;
+      m.skip0 = PSORT && ((gu >> 30) & 1u) != 0;
       const bool live = q != kNoSet && !m.slow;
       voff0 = live ? r.y + 16u * L.col : kV8Oob;
       return r.x & 0x7FFFFFu;
@@ -420,6 +446,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     m.Jset = min(jmax, (uint32_t)JM);
     m.mixed = jmin != jmax;
     m.g1 = __builtin_amdgcn_ballot_w64(pad > 256u) != 0;
+    m.skip0 = false;
     const bool live = q != kNoSet && !m.slow;
     voff0 = live ? wrel + 16u * L.col : kV8Oob;
     return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | ((r.w & 63u) << 16) |
@@ -505,9 +532,10 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     for (int j = 0; j < JM; j++) {
       if ((uint32_t)j < m.Jset) {
         if (m.mixed)
-          block8<true>(L, (uint32_t)j, J, pad, t, m.g1, false, b.x[2 * j], b.x[2 * j + 1], c);
+          block8<true>(L, (uint32_t)j, J, pad, t, m.g1, false, b.x[2 * j], b.x[2 * j + 1], c, m.skip0);
         else
-          block8<false>(L, (uint32_t)j, J, pad, t, m.g1, (uint32_t)j + 1 == m.Jset, b.x[2 * j], b.x[2 * j + 1], c);
+          block8<false>(L, (uint32_t)j, J, pad, t, m.g1, (uint32_t)j + 1 == m.Jset, b.x[2 * j], b.x[2 * j + 1], c,
+                        m.skip0);
       }
     }
     finish(q, geo, c, voff0, sb);
@@ -681,6 +709,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 UFC_V8_INSTG(false, false) UFC_V8_INSTG(true, false) UFC_V8_INSTG(false, true) UFC_V8_INSTG(true, true)
 #ifdef UFC_TUNING
 template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxFirstDefault, true>(const KernelParams);
+template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8Aux, true, true>(const KernelParams);
+template __global__ void frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8Aux, true, true>(const KernelParams);
 template __global__ void frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8AuxFirstDefault, true>(const KernelParams);
 UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
 UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
@@ -1079,6 +1109,10 @@ const void* stream8_kernel_symbol(bool seal) {
 const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux, bool geor) {
   if (geor) {
 #ifdef UFC_TUNING
+    if (insort && sortw == 64 && aux == kV8Aux && !pairs && std::getenv("UFC_V8_PSORT") &&
+        std::atoi(std::getenv("UFC_V8_PSORT")) != 0)  // A/B: P-sorted runs
+      return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8Aux, true, true>
+                  : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8Aux, true, true>;
     if (insort && sortw == 64 && aux == kV8AuxFirstDefault && !pairs)
       return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8AuxFirstDefault, true>
                   : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxFirstDefault, true>;
