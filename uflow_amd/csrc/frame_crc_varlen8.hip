@@ -30,8 +30,6 @@
 //     longer than 6 blocks, at the batch edges, past its end) run byte-wise, in the same loop.
 #include "frame_crc_dev.hpp"
 
-#include <cstdlib>
-
 namespace ufc_dev {
 
 namespace {
@@ -41,7 +39,6 @@ constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the se
 constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
 constexpr int kV8Aux = 0;                  // default cache policy (shared boundary lines)
-constexpr int kV8AuxFirstDefault = 100;    // (A/B) default policy for block 0, non-temporal for the rest
 constexpr uint32_t kNoSet = 0xFFFFFFFFu;   // a wave's set sequence past its last claimed run
 // The workgroup's run counter: nibble-image row 127, column 63 (columns 52..63 are never read).
 constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
@@ -131,7 +128,7 @@ __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
 // FREEZE: chains stop after the frame's own J blocks.
 template <bool FREEZE>
 __device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, uint32_t pad, uint32_t t, bool g1,
-                                       bool last_any, uint4 x0, uint4 x1, Chains& c, bool skip0 = false) {
+                                       bool last_any, uint4 x0, uint4 x1, Chains& c) {
   if (FREEZE ? (j + 1 == J) : last_any) {
     c.tr = t ? __builtin_amdgcn_alignbyte(x1.w, x1.z, 4u - t) : x1.w;
     if (L.col == 7u) {  // the trailer and the bytes past the frame are CRC'd as zeros
@@ -140,15 +137,8 @@ __device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, u
     }
   }
   if (j == 0) {
-    x1 = fix_piece(L.lds, x1, (int)pad - 128 - (int)(16u * L.col));
-    if (skip0) {  // (wave-uniform) A^128(0) ^ x1 = x1: no chain step on the zero first piece
-      c.v0 = x1.x;
-      c.v1 = x1.y;
-      c.v2 = x1.z;
-      c.v3 = x1.w;
-      return;
-    }
     const uint4 f0 = fix_piece(L.lds, x0, (int)pad - (int)(16u * L.col));
+    x1 = fix_piece(L.lds, x1, (int)pad - 128 - (int)(16u * L.col));
     c.v0 = f0.x;
     c.v1 = f0.y;
     c.v2 = f0.z;
@@ -179,7 +169,6 @@ struct Set8Meta {
   bool slow;      // byte path
   bool mixed;     // block counts differ
   bool g1;        // a frame's G straddles into block 1 (pad > 256)
-  bool skip0;     // (PSORT) every frame's first piece is zeros: the chains start at the second piece
 };
 
 template <int J>
@@ -200,11 +189,7 @@ struct Buf8 {
 // half-row DPP reductions and ballots; a set then takes its two words per group with ds_bpermute
 // and its set-level bits with one readfirstlane.  Frames the fast path cannot take sort together
 // (key 7), so they spoil fewer sets.
-// PSORT (with GEOR): runs sorted by 128-byte piece count P instead of block count J (sets then share
-// P as well as J), and a set whose frames all have >= 132 pad bytes -- its first piece is zeros in
-// every lane -- starts its chains at the second piece (no chain step on a zero state).
-template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux, bool GEOR = false,
-          bool PSORT = false>
+template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux, bool GEOR = false>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
   static_assert(SORTW == 8 || SORTW == 16 || SORTW == 32 || SORTW == 64, "sort window");
   static_assert(!GEOR || INSORT, "per-run geometry needs the in-kernel sort");
@@ -294,10 +279,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       sb = run_base(a);
       fg = frame_geo(a, len, live, sb);
       key = !live ? 8u : (fg.bad ? 7u : (uint32_t)J);
-      if constexpr (PSORT) {  // P = ceil((len + t + 4) / 128) = 2J or 2J - 1 (pad >= 128)
-        const uint32_t P = 2u * ((fg.geo >> 9) & 7u) - ((fg.geo & 511u) >= 128u ? 1u : 0u);
-        key = !live ? 14u : (fg.bad ? 13u : P);
-      }
     }
     if constexpr (SORTW == 8) {  // sets of consecutive frames: no reordering
       out.a_lo = (uint32_t)a;
@@ -308,9 +289,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     }
     const uint64_t qmask = SORTW == 64 ? ~0ull : (((1ull << SORTW) - 1ull) << (L.lane & ~(uint32_t)(SORTW - 1)));
     uint32_t below = 0, rank_in = 0;
-    constexpr uint32_t kMaxKey = PSORT ? 14u : 8u;
 #pragma unroll
-    for (uint32_t k = 1; k <= kMaxKey; k++) {
+    for (uint32_t k = 1; k <= 8; k++) {
       const uint64_t m = __builtin_amdgcn_ballot_w64(key == k) & qmask;
       below += (k < key) ? (uint32_t)__builtin_popcountll(m) : 0u;
       const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -336,13 +316,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
         const uint64_t mg1 = __builtin_amdgcn_ballot_w64((geo & 511u) > 256u);
         const uint32_t s8 = L.lane & ~7u;
         const uint32_t slow = ((mbad >> s8) & 0xFFu) != 0 ? 1u : 0u, g1 = ((mg1 >> s8) & 0xFFu) != 0 ? 1u : 0u;
-        uint32_t skip0 = 0;
-        if constexpr (PSORT) {  // every frame of the set: >= 132 pad bytes (piece 0 all zeros, G in piece 1)
-          const uint64_t mz = __builtin_amdgcn_ballot_w64((geo & 511u) >= 132u);
-          skip0 = ((mz >> s8) & 0xFFu) == 0xFFu ? 1u : 0u;
-        }
-        out.a_lo = geo | (min(jx, (uint32_t)JM) << 24) | ((jx != jn ? 1u : 0u) << 27) | (slow << 28) | (g1 << 29) |
-                   (skip0 << 30);
+        out.a_lo = geo | (min(jx, (uint32_t)JM) << 24) | ((jx != jn ? 1u : 0u) << 27) | (slow << 28) | (g1 << 29);
         return;
       }
     }
@@ -417,7 +391,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       m.mixed = ((gu >> 27) & 1u) != 0;
       m.slow = ((gu >> 28) & 1u) != 0;
       m.g1 = ((gu >> 29) & 1u) != 0;
-      m.skip0 = PSORT && ((gu >> 30) & 1u) != 0;
       const bool live = q != kNoSet && !m.slow;
       voff0 = live ? r.y + 16u * L.col : kV8Oob;
       return r.x & 0x7FFFFFu;
@@ -446,7 +419,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     m.Jset = min(jmax, (uint32_t)JM);
     m.mixed = jmin != jmax;
     m.g1 = __builtin_amdgcn_ballot_w64(pad > 256u) != 0;
-    m.skip0 = false;
     const bool live = q != kNoSet && !m.slow;
     voff0 = live ? wrel + 16u * L.col : kV8Oob;
     return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | ((r.w & 63u) << 16) |
@@ -468,15 +440,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       for (int h = 0; h < 2; h++) {
         uint32_t vo = base;
         if (j == 0) vo = (128u * h + 16u * L.col + 16u <= pad) ? kV8Oob : vo;
-        // AUX kV8AuxFirstDefault: default policy for block 0 (the lines a frame shares with the
-        // frame before it), non-temporal for the rest
-        u32x4 v;
-        if (AUX != kV8AuxFirstDefault)
-          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, AUX == kV8AuxFirstDefault ? 0 : AUX);
-        else if (j == 0)
-          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, 0);
-        else
-          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, 2);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, AUX);
         b.x[2 * j + h] = make_uint4(v.x, v.y, v.z, v.w);
       }
     }
@@ -532,10 +496,9 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
     for (int j = 0; j < JM; j++) {
       if ((uint32_t)j < m.Jset) {
         if (m.mixed)
-          block8<true>(L, (uint32_t)j, J, pad, t, m.g1, false, b.x[2 * j], b.x[2 * j + 1], c, m.skip0);
+          block8<true>(L, (uint32_t)j, J, pad, t, m.g1, false, b.x[2 * j], b.x[2 * j + 1], c);
         else
-          block8<false>(L, (uint32_t)j, J, pad, t, m.g1, (uint32_t)j + 1 == m.Jset, b.x[2 * j], b.x[2 * j + 1], c,
-                        m.skip0);
+          block8<false>(L, (uint32_t)j, J, pad, t, m.g1, (uint32_t)j + 1 == m.Jset, b.x[2 * j], b.x[2 * j + 1], c);
       }
     }
     finish(q, geo, c, voff0, sb);
@@ -708,10 +671,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 // kept for A/B in tuning builds.
 UFC_V8_INSTG(false, false) UFC_V8_INSTG(true, false) UFC_V8_INSTG(false, true) UFC_V8_INSTG(true, true)
 #ifdef UFC_TUNING
-template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxFirstDefault, true>(const KernelParams);
-template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8Aux, true, true>(const KernelParams);
-template __global__ void frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8Aux, true, true>(const KernelParams);
-template __global__ void frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8AuxFirstDefault, true>(const KernelParams);
 UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
 UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
 UFC_V8_INSTW(false, 8) UFC_V8_INSTW(false, 16) UFC_V8_INSTW(false, 32) UFC_V8_INSTW(true, 8) UFC_V8_INSTW(true, 16)
@@ -1108,15 +1067,6 @@ const void* stream8_kernel_symbol(bool seal) {
 
 const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux, bool geor) {
   if (geor) {
-#ifdef UFC_TUNING
-    if (insort && sortw == 64 && aux == kV8Aux && !pairs && std::getenv("UFC_V8_PSORT") &&
-        std::atoi(std::getenv("UFC_V8_PSORT")) != 0)  // A/B: P-sorted runs
-      return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8Aux, true, true>
-                  : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8Aux, true, true>;
-    if (insort && sortw == 64 && aux == kV8AuxFirstDefault && !pairs)
-      return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8AuxFirstDefault, true>
-                  : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxFirstDefault, true>;
-#endif
     if (!insort || sortw != 64 || aux != kV8Aux) return nullptr;
     if (pairs)
       return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true, 64, kV8Aux, true>

@@ -180,7 +180,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
 // is a dependent load chain per frame, bound by how many chains are in flight).  A frame that finds
 // the pool full is walked again by the emit step, as one with more than kPosSlots datagrams.
 constexpr uint32_t kInlineSlots = 16;
-constexpr uint32_t kPoolSlots = 2036;  // (2036 rather than 2048: the SORT walk then fits 8 workgroups per CU)
+constexpr uint32_t kPoolSlots = 2048;
 constexpr uint32_t kPoolNil = 0xFFFFu;
 
 struct PoolSink {
@@ -213,13 +213,6 @@ struct PoolSink {
   }
 };
 
-// SORT: the workgroup's frames are handed to its threads in order of their datagram count, read
-// from each frame's first 8 bytes before the walk (a data frame's count byte; 0 for every other
-// kind: acks sit at fixed offsets and walk nothing), so that the 64 lanes of a wave walk chains of
-// similar length: a wave's loop runs to its longest chain, and in a mixed batch (data frames of
-// 0..63 datagrams beside acks and short frames) the unsorted waves ran ~4x more iterations than
-// their lanes needed.  The header slots still leave in frame order (a scan over the frames).
-template <bool SORT>
 __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const uint8_t* bytes, const uint64_t* offsets,
                                                                         uint64_t n, const uint8_t* valid,
                                                                         ufc_frame_info* infos, uint32_t* counts,
@@ -230,42 +223,10 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   __shared__ uint32_t pool[kPoolSlots];
   __shared__ typename BlockScan::TempStorage scan_tmp;
   __shared__ uint32_t base_lds, pool_ctr;
-  // SORT: the frames' first 8 bytes (then, after the walk, each frame's first slot), the thread ->
-  // frame map, and the count histogram (then each frame's slot count)
-  __shared__ uint64_t s_head8[SORT ? kParseThreads : 1];
-  __shared__ uint16_t s_perm[SORT ? kParseThreads : 1];
-  __shared__ uint16_t s_hist[SORT ? kParseThreads : 1];
   const uint32_t t = threadIdx.x;
-  const uint64_t i0 = (uint64_t)blockIdx.x * kParseThreads;
+  const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + t;
   if (t == 0) pool_ctr = 0;
-  uint32_t tf = t;  // the frame (of the workgroup) this thread walks
-  if constexpr (SORT) {
-    if (t < 64) ((uint32_t*)s_hist)[t] = 0;  // the 128 16-bit counters
-    uint64_t w = 0;
-    uint32_t key = 0;
-    if (i0 + t < n) {
-      uint64_t a;
-      const uint32_t len = frame_len32(offsets, i0 + t, a);
-      if (len >= 8) w = DevBytesHead::load8(bytes + a);
-      if (valid[i0 + t] != 0 && len >= 8 && (w & 0xFFu) == UFC_FRAME_DATA) key = (uint32_t)(w >> 40) & 0x7Fu;
-    }
-    s_head8[t] = w;
-    __syncthreads();
-    // (LDS atomic on a 16-bit counter: the 16-bit word's own dword, so no neighbour is touched)
-    const uint32_t r = atomicAdd((uint32_t*)s_hist + (key >> 1), 1u << (16 * (key & 1))) >> (16 * (key & 1)) & 0xFFFFu;
-    __syncthreads();
-    uint32_t first_of_key;
-    BlockScan(scan_tmp).ExclusiveSum(t < 128 ? s_hist[t] : 0u, first_of_key);
-    __syncthreads();
-    if (t < 128) s_hist[t] = (uint16_t)first_of_key;
-    __syncthreads();
-    s_perm[s_hist[key] + r] = (uint16_t)t;
-    __syncthreads();
-    tf = s_perm[t];
-  } else {
-    __syncthreads();
-  }
-  const uint64_t i = i0 + tf;
+  __syncthreads();
   uint32_t npos = 0, head = kPoolNil, tail = kPoolNil;
   bool full = false;
   uint8_t mode = kItemsNone;
@@ -274,7 +235,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
     const bool has8 = len >= 8;
-    const DevBytesHead rd{bytes + a, has8 ? (SORT ? s_head8[tf] : DevBytesHead::load8(bytes + a)) : 0ull, has8};
+    const DevBytesHead rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8};
     const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
     const uint32_t cnt = ok ? info.item_count : 0u;
@@ -293,18 +254,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     counts[i] = cnt;
   }
   uint32_t lo, total;
-  if constexpr (SORT) {  // the slots leave in frame order: scan the slot counts over the frames
-    __syncthreads();     // (every thread is past its reads of s_hist / s_head8)
-    s_hist[tf] = (uint16_t)npos;
-    __syncthreads();
-    uint32_t lo_f;
-    BlockScan(scan_tmp).ExclusiveSum(s_hist[t], lo_f, total);
-    ((uint32_t*)s_head8)[t] = lo_f;
-    __syncthreads();
-    lo = ((uint32_t*)s_head8)[tf];
-  } else {
-    BlockScan(scan_tmp).ExclusiveSum(npos, lo, total);
-  }
+  BlockScan(scan_tmp).ExclusiveSum(npos, lo, total);
   if (t == 0) {
     // (64-bit cursor: the sum of every workgroup's total may pass 2^32 long after the cap is reached)
     const unsigned long long b64 = total ? atomicAdd(seg_cursor, (unsigned long long)total) : 0ull;
@@ -516,14 +466,13 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   hipError_t e = hipMemsetAsync(cursor, 0, 8, stream);
   if (e != hipSuccess) return e;
   bool pool = true;  // pooled header slots (more walking frames per CU); UFC_WALK_POOL=0 (tuning): fixed slots
-  bool sort = false;  // frames handed to threads by datagram count; UFC_WALK_SORT (tuning A/B)
 #ifdef UFC_TUNING
   if (const char* w = std::getenv("UFC_WALK_POOL")) pool = std::atoi(w) != 0;
-  if (const char* w = std::getenv("UFC_WALK_SORT")) sort = std::atoi(w) != 0;
 #endif
   if (pool)
-    (sort ? parse_walk_pool_kernel<true> : parse_walk_pool_kernel<false>)<<<(unsigned)blocks, kParseThreads, 0, stream>>>(
-        a.bytes, a.offsets, n, a.valid, a.infos, counts, modes, pos_seg, cursor, bases, lay.seg_cap);
+    parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
+                                                                           counts, modes, pos_seg, cursor, bases,
+                                                                           lay.seg_cap);
   else
     parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
                                                                       modes, pos_seg, cursor, bases, lay.seg_cap);
