@@ -248,12 +248,19 @@ def launch_ranks(a):
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=dict(os.environ))
     lines = []
     for line in p.stdout:
-        try:
-            j = json.loads(line)
-        except ValueError:
-            j = None
+        # (ranks share the launcher's stdout: another rank's unterminated print may precede the JSON
+        # object on the same line, so the object is looked for anywhere in the line)
+        k = line.find('{"metric"')
+        j = None
+        if k >= 0:
+            try:
+                j = json.loads(line[k:])
+            except ValueError:
+                j = None
         if isinstance(j, dict) and "metric" in j:
-            lines.append(line.strip())
+            if k > 0:
+                sys.stderr.write(line[:k] + "\n")
+            lines.append(line[k:].strip())
         else:
             sys.stderr.write(line)
             sys.stderr.flush()
