@@ -6,7 +6,7 @@ TAG=${1:-pmclean}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
-export TMPDIR=/tmp UFC_LIB=$R/uflow_amd/libuflowcrc_tuning.so
+export TMPDIR=/tmp UFC_LIB=${UFC_LIB:-$R/uflow_amd/libuflowcrc_tuning.so}
 shift
 timeout -k 10 60 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 for ab in ${ABS:-0 1}; do
