@@ -513,7 +513,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8> (ufc_crc_batch_fixed"
+                "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8, 4224> (ufc_crc_batch_fixed"
                           + (", per chunk of ufc_crc_sharded" if sharded else "") + ")",
                 "kernel_avg_ms": round(kern_ms, 4),
                 "kernel_median_ms": round(float(np.median(kern_all)), 4),

@@ -113,7 +113,7 @@ def main():
         json.dump(summary, f, indent=1)
     b = summary.get("config 2 validate (bench line)")
     if b and b["fetch_bytes_per_dispatch"] and b["write_bytes_per_dispatch"]:
-        out = {"frames": N2, "frame_len": L2, "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8>",
+        out = {"frames": N2, "frame_len": L2, "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8, 4224>",
                "fetch_bytes_per_launch": b["fetch_bytes_per_dispatch"],
                "write_bytes_per_launch": b["write_bytes_per_dispatch"],
                "hbm_bytes_per_launch": b["fetch_bytes_per_dispatch"] + b["write_bytes_per_dispatch"],

@@ -362,7 +362,7 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 // 0 wholly before G load nothing (an out-of-range offset: zeros, no memory request; the front fix
 // zeroes them anyway).  The lines a frame shares with its neighbours sit in its first and last block.
 constexpr int lean_loadv(int skip, int first, int mid, int last) { return skip | first << 1 | mid << 6 | last << 11; }
-constexpr int kLoadvAllNT = lean_loadv(0, kFixAuxNT, kFixAuxNT, kFixAuxNT);  // rounds 1-3
+[[maybe_unused]] constexpr int kLoadvAllNT = lean_loadv(0, kFixAuxNT, kFixAuxNT, kFixAuxNT);  // rounds 1-3 (A/B)
 // Product (round 4): default policy for block 0, non-temporal for the rest: 0.2277-0.2289 against
 // 0.2372-0.2383 ms per 1M x 1500 B (in-process A/B, identical results; profiles/EXPERIMENTS.md).
 constexpr int kLoadvProduct = lean_loadv(0, 0, kFixAuxNT, kFixAuxNT);

@@ -39,8 +39,6 @@ constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the se
 constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
 constexpr int kV8Aux = 0;                  // default cache policy (shared boundary lines)
-// (A/B) blocks 1 .. kV8AuxNT1 - 100 non-temporal, the rest default: static, whatever the set's block count
-constexpr int kV8AuxNT1 = 101, kV8AuxNT2 = 102, kV8AuxNT3 = 103;
 constexpr uint32_t kNoSet = 0xFFFFFFFFu;   // a wave's set sequence past its last claimed run
 // The workgroup's run counter: nibble-image row 127, column 63 (columns 52..63 are never read).
 constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
@@ -442,11 +440,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       for (int h = 0; h < 2; h++) {
         uint32_t vo = base;
         if (j == 0) vo = (128u * h + 16u * L.col + 16u <= pad) ? kV8Oob : vo;
-        u32x4 v;
-        if (AUX >= kV8AuxNT1 && AUX <= kV8AuxNT3 && j >= 1 && j <= AUX - 100)
-          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, 2);
-        else
-          v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, AUX >= 100 ? 0 : AUX);
+        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, AUX);
         b.x[2 * j + h] = make_uint4(v.x, v.y, v.z, v.w);
       }
     }
@@ -677,9 +671,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
 // kept for A/B in tuning builds.
 UFC_V8_INSTG(false, false) UFC_V8_INSTG(true, false) UFC_V8_INSTG(false, true) UFC_V8_INSTG(true, true)
 #ifdef UFC_TUNING
-template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxNT1, true>(const KernelParams);
-template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxNT2, true>(const KernelParams);
-template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxNT3, true>(const KernelParams);
 UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
 UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
 UFC_V8_INSTW(false, 8) UFC_V8_INSTW(false, 16) UFC_V8_INSTW(false, 32) UFC_V8_INSTW(true, 8) UFC_V8_INSTW(true, 16)
@@ -1076,12 +1067,6 @@ const void* stream8_kernel_symbol(bool seal) {
 
 const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux, bool geor) {
   if (geor) {
-#ifdef UFC_TUNING
-    if (insort && sortw == 64 && !pairs && !seal && aux >= kV8AuxNT1 && aux <= kV8AuxNT3)
-      return aux == kV8AuxNT1   ? (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxNT1, true>
-             : aux == kV8AuxNT2 ? (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxNT2, true>
-                                : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8AuxNT3, true>;
-#endif
     if (!insort || sortw != 64 || aux != kV8Aux) return nullptr;
     if (pairs)
       return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true, 64, kV8Aux, true>
