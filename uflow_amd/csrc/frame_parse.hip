@@ -79,6 +79,35 @@ struct DevBytesHead {
   }
 };
 
+// The walk's reader with a prefetch PF bytes ahead of each datagram header (PF > 0): with each
+// header's dword load goes a load PF bytes further into the frame, whose value is never used (folded
+// into a register the asm below keeps alive), so that the line the next header most likely sits in
+// is on its way to L2 while this header is decoded.  The previous prefetch is folded in after the
+// next header's load is issued: it is older than that load, so waiting for the header waits for it
+// too and the fold never adds a wait.
+template <int PF>
+struct DevBytesHeadPF {
+  const uint8_t* p;
+  uint64_t w;  // bytes 0..7, little-endian
+  bool has8;
+  uint32_t lim;   // the last dword start inside the frame (len - 4)
+  uint32_t* pf;   // the previous prefetch's value
+  uint32_t* sink;
+  __device__ uint32_t operator()(uint32_t i) const {
+    if (has8 && i < 8) return (uint32_t)(w >> (8 * i)) & 0xFFu;
+    return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
+  }
+  __device__ uint32_t head3(uint32_t i) const {
+    const uint32_t v = *(g_u32_a1*)(p + i);
+    if constexpr (PF > 0) {
+      const uint32_t f = *(g_u32_a1*)(p + min(i + (uint32_t)PF, lim));
+      *sink ^= *pf;
+      *pf = f;
+    }
+    return v & 0xFFFFFFu;
+  }
+};
+
 // Walk sink: only the header offsets, into this thread's LDS slots (slot k at k * kParseThreads).
 struct PosSink {
   static constexpr bool kDecode = false;
@@ -213,6 +242,7 @@ struct PoolSink {
   }
 };
 
+template <int PF>
 __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const uint8_t* bytes, const uint64_t* offsets,
                                                                         uint64_t n, const uint8_t* valid,
                                                                         ufc_frame_info* infos, uint32_t* counts,
@@ -235,9 +265,15 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
     const bool has8 = len >= 8;
-    const DevBytesHead rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8};
+    uint32_t pf = 0, sink = 0;
+    const DevBytesHeadPF<PF> rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8, len >= 4 ? len - 4u : 0u,
+                                &pf, &sink};
     const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
+    if constexpr (PF > 0) {
+      sink ^= pf;
+      asm volatile("" : : "v"(sink));  // (keeps the prefetch loads)
+    }
     const uint32_t cnt = ok ? info.item_count : 0u;
     if (cnt) {
       if (info.kind == UFC_FRAME_ACK) {
@@ -466,13 +502,16 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   hipError_t e = hipMemsetAsync(cursor, 0, 8, stream);
   if (e != hipSuccess) return e;
   bool pool = true;  // pooled header slots (more walking frames per CU); UFC_WALK_POOL=0 (tuning): fixed slots
+  int pf = 0;        // prefetch distance of the walk's reader (UFC_WALK_PF, tuning A/B)
 #ifdef UFC_TUNING
   if (const char* w = std::getenv("UFC_WALK_POOL")) pool = std::atoi(w) != 0;
+  if (const char* w = std::getenv("UFC_WALK_PF")) pf = std::atoi(w);
 #endif
+  auto walk = pf == 64 ? parse_walk_pool_kernel<64> : pf == 128 ? parse_walk_pool_kernel<128>
+              : pf == 256 ? parse_walk_pool_kernel<256> : parse_walk_pool_kernel<0>;
   if (pool)
-    parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
-                                                                           counts, modes, pos_seg, cursor, bases,
-                                                                           lay.seg_cap);
+    walk<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts, modes, pos_seg,
+                                                         cursor, bases, lay.seg_cap);
   else
     parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
                                                                       modes, pos_seg, cursor, bases, lay.seg_cap);
