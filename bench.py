@@ -232,6 +232,21 @@ def shard_reference(frames, n, L, threads, chunk=1 << 20):
     return ref_crc, ref_valid
 
 
+def split_result_line(line):
+    """(text before, rank 0's JSON result) if the line holds the result object, else (line, None).  Ranks
+    share the launcher's stdout, so another rank's unterminated print may precede the object on the same
+    line: the object is looked for anywhere in the line."""
+    k = line.find('{"metric"')
+    if k >= 0:
+        try:
+            j = json.loads(line[k:])
+        except ValueError:
+            j = None
+        if isinstance(j, dict) and "metric" in j:
+            return line[:k], line[k:].strip()
+    return line, None
+
+
 def launch_ranks(a):
     """--gpus N > 1 without a launcher: run N ranks of this script under torch.distributed.run as a
     child process (this process makes no GPU call), forward rank 0's JSON line to stdout (other
@@ -248,19 +263,11 @@ def launch_ranks(a):
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=dict(os.environ))
     lines = []
     for line in p.stdout:
-        # (ranks share the launcher's stdout: another rank's unterminated print may precede the JSON
-        # object on the same line, so the object is looked for anywhere in the line)
-        k = line.find('{"metric"')
-        j = None
-        if k >= 0:
-            try:
-                j = json.loads(line[k:])
-            except ValueError:
-                j = None
-        if isinstance(j, dict) and "metric" in j:
-            if k > 0:
-                sys.stderr.write(line[:k] + "\n")
-            lines.append(line[k:].strip())
+        before, obj = split_result_line(line)
+        if obj is not None:
+            if before:
+                sys.stderr.write(before + "\n")
+            lines.append(obj)
         else:
             sys.stderr.write(line)
             sys.stderr.flush()

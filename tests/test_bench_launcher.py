@@ -32,3 +32,13 @@ def test_bench_launcher_three_ranks():
     assert p.returncode == 0, p.stderr[-2000:]
     j = json.loads(p.stdout.strip())
     assert j["ranks_seen"] == 3
+
+
+def test_split_result_line_interleaved():
+    """Rank 0's JSON line found when another rank's print landed in front of it on the same line."""
+    import bench
+    obj = '{"metric": "m", "value": 1}'
+    assert bench.split_result_line(obj + "\n") == ("", obj)
+    assert bench.split_result_line("rank 2 of 3 alive" + obj + "\n") == ("rank 2 of 3 alive", obj)
+    assert bench.split_result_line("rank 1 of 3 alive\n") == ("rank 1 of 3 alive\n", None)
+    assert bench.split_result_line('{"metric": broken\n')[1] is None
