@@ -79,35 +79,6 @@ struct DevBytesHead {
   }
 };
 
-// The walk's reader with a prefetch PF bytes ahead of each datagram header (PF > 0): with each
-// header's dword load goes a load PF bytes further into the frame, whose value is never used (folded
-// into a register the asm below keeps alive), so that the line the next header most likely sits in
-// is on its way to L2 while this header is decoded.  The previous prefetch is folded in after the
-// next header's load is issued: it is older than that load, so waiting for the header waits for it
-// too and the fold never adds a wait.
-template <int PF>
-struct DevBytesHeadPF {
-  const uint8_t* p;
-  uint64_t w;  // bytes 0..7, little-endian
-  bool has8;
-  uint32_t lim;   // the last dword start inside the frame (len - 4)
-  uint32_t* pf;   // the previous prefetch's value
-  uint32_t* sink;
-  __device__ uint32_t operator()(uint32_t i) const {
-    if (has8 && i < 8) return (uint32_t)(w >> (8 * i)) & 0xFFu;
-    return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
-  }
-  __device__ uint32_t head3(uint32_t i) const {
-    const uint32_t v = *(g_u32_a1*)(p + i);
-    if constexpr (PF > 0) {
-      const uint32_t f = *(g_u32_a1*)(p + min(i + (uint32_t)PF, lim));
-      *sink ^= *pf;
-      *pf = f;
-    }
-    return v & 0xFFFFFFu;
-  }
-};
-
 // Walk sink: only the header offsets, into this thread's LDS slots (slot k at k * kParseThreads).
 struct PosSink {
   static constexpr bool kDecode = false;
@@ -242,7 +213,6 @@ struct PoolSink {
   }
 };
 
-template <int PF>
 __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const uint8_t* bytes, const uint64_t* offsets,
                                                                         uint64_t n, const uint8_t* valid,
                                                                         ufc_frame_info* infos, uint32_t* counts,
@@ -265,15 +235,9 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
     const bool has8 = len >= 8;
-    uint32_t pf = 0, sink = 0;
-    const DevBytesHeadPF<PF> rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8, len >= 4 ? len - 4u : 0u,
-                                &pf, &sink};
+    const DevBytesHead rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8};
     const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
-    if constexpr (PF > 0) {
-      sink ^= pf;
-      asm volatile("" : : "v"(sink));  // (keeps the prefetch loads)
-    }
     const uint32_t cnt = ok ? info.item_count : 0u;
     if (cnt) {
       if (info.kind == UFC_FRAME_ACK) {
@@ -314,115 +278,11 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   }
 }
 
-// ---- STAGE (tuning A/B): the walk decodes every datagram itself and stages its item ----
-// The walk's reader loads each header as 16 bytes (one unaligned dwordx4: a datagram header is at most
-// 14 bytes) instead of its 3 size bytes, so the header is in registers when the codec reports it; the
-// sink decodes the item there and stores it at stage[frame * kPosSlots + k] (24 bytes, three dwordx2
-// stores hidden from the compiler's wait counts: the next header's load then never waits for them,
-// see frame_crc_dev.hpp).  The emit step only copies a staged frame's items to their place in frame
-// order (no header reads), and walks frames with more than kPosSlots datagrams or acks as before.
-template <int PF>
-struct DevBytesHeadStage {
-  const uint8_t* p;
-  uint64_t w;  // bytes 0..7, little-endian
-  bool has8;
-  uint32_t lim;   // the last dword start inside the frame (len - 4)
-  uint32_t lim16; // the last 16-byte window start inside the frame (len - 16), or 0 (short frame)
-  uint32_t* win;  // the last header's 16 bytes
-  uint32_t* pf;   // the previous prefetch's value
-  uint32_t* sink;
-  __device__ uint32_t operator()(uint32_t i) const {
-    if (has8 && i < 8) return (uint32_t)(w >> (8 * i)) & 0xFFu;
-    return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
-  }
-  __device__ uint32_t head3(uint32_t i) const {
-    // 16 bytes from i (any alignment); near the frame's end the window starts earlier and the bytes
-    // are shifted into place (a header never extends past the frame: the codec checks rem >= hs + dl)
-    uint32_t x[4];
-    if (i <= lim16 && lim16 != 0) {  // the 16 bytes lie inside the frame: one load
-      typedef unsigned int v4 __attribute__((ext_vector_type(4)));
-      typedef const __attribute__((address_space(1), aligned(1))) v4 g_v4_a1;
-      const v4 v = *(g_v4_a1*)(p + i);
-      x[0] = v.x, x[1] = v.y, x[2] = v.z, x[3] = v.w;
-    } else {  // within 16 bytes of the frame's end: the bytes that exist, one by one
-#pragma unroll
-      for (int q = 0; q < 4; q++) x[q] = 0;
-#pragma unroll
-      for (uint32_t c = 0; c < 16; c++)
-        if (i + c < lim + 4u) x[c >> 2] |= (uint32_t)*(const __attribute__((address_space(1))) uint8_t*)(p + i + c) << (8 * (c & 3));
-    }
-#pragma unroll
-    for (int q = 0; q < 4; q++) win[q] = x[q];
-    if constexpr (PF > 0) {
-      const uint32_t f = *(g_u32_a1*)(p + min(i + (uint32_t)PF, lim));
-      *sink ^= *pf;
-      *pf = f;
-    }
-    return x[0] & 0xFFFFFFu;
-  }
-};
-
-__device__ __forceinline__ void st_u64_hidden(uint64_t* a, uint64_t v) {
-  asm volatile("global_store_dwordx2 %0, %1, off" : : "v"(a), "v"(v));
-}
-
-struct StageSink {
-  static constexpr bool kDecode = false;
-  uint64_t* dst;          // this frame's kPosSlots staged items (3 words each)
-  const uint32_t* win;    // the reader's last header window
-  __device__ bool on() const { return true; }
-  __device__ void operator()(uint32_t, const ufc_item&) const {}
-  __device__ void header(uint32_t k, uint32_t off) const {
-    if (k >= kPosSlots) return;
-    auto h = [&](uint32_t c) -> uint32_t { return (win[c >> 2] >> (8 * (c & 3))) & 0xFFu; };
-    uint32_t hs, dl;
-    ufc_codec::datagram_size(h, hs, dl);
-    ufc_item it{};
-    ufc_codec::decode_datagram(h, hs, it);
-    it.data_offset = off + hs;
-    uint64_t* q = dst + 3 * k;
-    st_u64_hidden(q, (uint64_t)it.id | ((uint64_t)it.channel_id << 32) | ((uint64_t)it.form << 40) |
-                         ((uint64_t)it.window_parent_lead << 48));
-    st_u64_hidden(q + 1, (uint64_t)it.channel_parent_lead | ((uint64_t)it.fragment_id << 16) |
-                             ((uint64_t)it.fragment_id_last << 32) | ((uint64_t)it.flags << 48));
-    st_u64_hidden(q + 2, (uint64_t)it.data_offset | ((uint64_t)it.data_len << 32));
-  }
-};
-
-template <int PF>
-__global__ __launch_bounds__(kParseThreads) void parse_walk_stage_kernel(const uint8_t* bytes, const uint64_t* offsets,
-                                                                         uint64_t n, const uint8_t* valid,
-                                                                         ufc_frame_info* infos, uint32_t* counts,
-                                                                         uint8_t* modes, uint64_t* stage) {
-  const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + threadIdx.x;
-  if (i >= n) return;
-  uint64_t a;
-  const uint32_t len = frame_len32(offsets, i, a);
-  ufc_frame_info info;
-  const bool has8 = len >= 8;
-  uint32_t pf = 0, sink = 0, win[4] = {0u, 0u, 0u, 0u};
-  const DevBytesHeadStage<PF> rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8,
-                                 len >= 4 ? len - 4u : 0u, len >= 16 ? len - 16u : 0u, win, &pf, &sink};
-  const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info, StageSink{stage + 3 * kPosSlots * i, win},
-                                           kPosSlots);
-  if constexpr (PF > 0) {
-    sink ^= pf;
-    asm volatile("" : : "v"(sink));  // (keeps the prefetch loads)
-  }
-  const uint32_t cnt = ok ? info.item_count : 0u;
-  uint8_t mode = kItemsNone;
-  if (cnt) mode = info.kind == UFC_FRAME_ACK ? kItemsAck : (cnt <= kPosSlots ? kItemsPos : kItemsWalk);
-  info.item_first = 0;  // written by the emit step
-  infos[i] = info;
-  counts[i] = cnt;
-  modes[i] = mode;
-}
-
-template <int U, bool X4, bool STAGE = false>
+template <int U, bool X4>
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
     const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
-    const uint32_t* seg_base, ufc_item* items, uint64_t cap, uint64_t* items_used, const uint64_t* stage = nullptr) {
+    const uint32_t* seg_base, ufc_item* items, uint64_t cap, uint64_t* items_used) {
   __shared__ uint32_t lfirst[kParseThreads], lseg[kParseThreads];
   __shared__ uint64_t lstart[kParseThreads];
   __shared__ uint8_t lmode[kParseThreads];
@@ -464,7 +324,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
       __builtin_amdgcn_make_buffer_rsrc((void*)(base_addr - delta), 0, buf_ok ? (int)(uint32_t)range : 0, 0x00020000);
 
   const uint32_t g0 = lfirst[0], g1 = lend;
-  const uint32_t sb = STAGE ? 0xFFFFFFFFu : seg_base[blockIdx.x];  // (0xFFFFFFFF: no segment, and no kItemsPos frame either)
+  const uint32_t sb = seg_base[blockIdx.x];  // (0xFFFFFFFF: no segment, and no kItemsPos frame either)
   const uint16_t* seg = pos_seg + (sb == 0xFFFFFFFFu ? 0u : sb);
   if (items) {
     // U items per thread per round (items g, g + 256, ...): every header load of the round is issued
@@ -490,16 +350,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
           }
           const uint32_t f = lo_f, k = (uint32_t)g - lfirst[f];
           const uint8_t m = lmode[f];
-          if (STAGE && m == kItemsPos) {  // staged by the walk: copy
-            const __attribute__((address_space(1))) uint64_t* q =
-                (const __attribute__((address_space(1))) uint64_t*)(stage + 3 * ((i0 + f) * kPosSlots + k));
-            typedef __attribute__((address_space(1))) uint64_t g_u64w;
-            g_u64w* o = (g_u64w*)(items + g);
-            const uint64_t q0 = q[0], q1 = q[1], q2 = q[2];
-            o[0] = q0;
-            o[1] = q1;
-            o[2] = q2;
-          } else if (m == kItemsPos || m == kItemsAck) {
+          if (m == kItemsPos || m == kItemsAck) {
             mm[u] = m;
             fo[u] = f;
             hoff[u] = m == kItemsPos ? (uint32_t)seg[lseg[f] + k]
@@ -569,8 +420,8 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
 
 namespace {
 struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned parts)
-  uint64_t counts, firsts, modes, cursor, bases, slots, temp, stage, end, seg_cap;
-  ParseLayout(uint64_t n, uint64_t items_cap, size_t temp_bytes, bool staged = false) {
+  uint64_t counts, firsts, modes, cursor, bases, slots, temp, end, seg_cap;
+  ParseLayout(uint64_t n, uint64_t items_cap, size_t temp_bytes) {
     auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
     const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
     // u16 header slots; below 2^32 - 1 so that every segment fits 32-bit offsets and no segment base
@@ -584,8 +435,7 @@ struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned pa
     bases = cursor + 256;
     slots = bases + up(blocks * 4);
     temp = slots + up(seg_cap * 2);
-    stage = temp + up(temp_bytes);  // STAGE: kPosSlots staged items of 24 bytes per frame
-    end = stage + (staged ? up(n * kPosSlots * 24) : 0);
+    end = temp + up(temp_bytes);
   }
 };
 size_t scan_temp_bytes(uint64_t n) {
@@ -595,22 +445,14 @@ size_t scan_temp_bytes(uint64_t n) {
 }
 }  // namespace
 
-bool parse_staged() {  // STAGE (UFC_PARSE_STAGE, tuning A/B)
-#ifdef UFC_TUNING
-  if (const char* w = std::getenv("UFC_PARSE_STAGE")) return std::atoi(w) != 0;
-#endif
-  return false;
-}
-
 size_t parse_scratch_bytes(uint64_t n, uint64_t items_cap) {
-  return ParseLayout(n, items_cap, scan_temp_bytes(n), parse_staged()).end;
+  return ParseLayout(n, items_cap, scan_temp_bytes(n)).end;
 }
 
 hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, hipStream_t stream) {
   const uint64_t n = a.n;
   const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
-  const bool staged = parse_staged();
-  const ParseLayout lay(n, a.items_cap, scan_temp_bytes(n), staged);
+  const ParseLayout lay(n, a.items_cap, scan_temp_bytes(n));
   if (lay.end > scratch_bytes) return hipErrorInvalidValue;
   char* s = (char*)scratch;
   uint32_t* counts = (uint32_t*)(s + lay.counts);
@@ -620,24 +462,17 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   uint32_t* bases = (uint32_t*)(s + lay.bases);
   uint16_t* pos_seg = (uint16_t*)(s + lay.slots);
   void* temp = s + lay.temp;
-  size_t temp_bytes = lay.stage - lay.temp;
-  uint64_t* stage = (uint64_t*)(s + lay.stage);
+  size_t temp_bytes = lay.end - lay.temp;
   hipError_t e = hipMemsetAsync(cursor, 0, 8, stream);
   if (e != hipSuccess) return e;
   bool pool = true;  // pooled header slots (more walking frames per CU); UFC_WALK_POOL=0 (tuning): fixed slots
-  int pf = 0;        // prefetch distance of the walk's reader (UFC_WALK_PF, tuning A/B)
 #ifdef UFC_TUNING
   if (const char* w = std::getenv("UFC_WALK_POOL")) pool = std::atoi(w) != 0;
-  if (const char* w = std::getenv("UFC_WALK_PF")) pf = std::atoi(w);
 #endif
-  auto walk = pf == 64 ? parse_walk_pool_kernel<64> : pf == 128 ? parse_walk_pool_kernel<128>
-              : pf == 256 ? parse_walk_pool_kernel<256> : parse_walk_pool_kernel<0>;
-  if (staged)
-    (pf == 128 ? parse_walk_stage_kernel<128> : parse_walk_stage_kernel<0>)<<<(unsigned)blocks, kParseThreads, 0, stream>>>(
-        a.bytes, a.offsets, n, a.valid, a.infos, counts, modes, stage);
-  else if (pool)
-    walk<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts, modes, pos_seg,
-                                                         cursor, bases, lay.seg_cap);
+  if (pool)
+    parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
+                                                                           counts, modes, pos_seg, cursor, bases,
+                                                                           lay.seg_cap);
   else
     parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
                                                                       modes, pos_seg, cursor, bases, lay.seg_cap);
@@ -659,13 +494,9 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
     else if (!x4) emit = parse_emit_kernel<1, false>;
   }
 #endif
-  if (staged)
-    parse_emit_kernel<1, true, true><<<(unsigned)blocks, kParseThreads, 0, stream>>>(
-        a.bytes, a.offsets, n, a.valid, a.infos, counts, firsts, modes, pos_seg, bases, a.items, a.items_cap,
-        a.items_used, stage);
-  else
-    emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts, firsts, modes,
-                                                         pos_seg, bases, a.items, a.items_cap, a.items_used, nullptr);
+  emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
+                                                                    firsts, modes, pos_seg, bases, a.items, a.items_cap,
+                                                                    a.items_used);
   return hipGetLastError();
 }
 
