@@ -100,9 +100,9 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 #define UFC_VARLEN_SORTED 2      /*   (tuning) round-1 kernel on frames sorted by block count within runs of 64 */
 #define UFC_VARLEN_BLOCKED8 3    /*   (tuning) round-1 kernel, static blocked schedule at 8 waves */
 #define UFC_VARLEN_CLAIM16 4     /*   (tuning) round-1 kernel, claimed sets at 16 waves (round-1 default) */
-#define UFC_VARLEN_BLOCKSTREAM 5 /*   (tuning) sorted block-stream kernel (one 1-KB block step at a time) */
+#define UFC_VARLEN_BLOCKSTREAM 5 /*   (removed in round 4, rejected: the block-stream kernel, measured slower) */
 #define UFC_VARLEN_SORTED8 6     /*   runs of 64 sorted in the kernel, 8-frame sets of 8 lanes per frame */
-#define UFC_VARLEN_STREAM 7      /*   (tuning) byte-balanced streams: 8-lane groups walk equal byte ranges (CSR) */
+#define UFC_VARLEN_STREAM 7      /*   (removed in round 4, rejected: the byte-balanced stream kernel, measured slower) */
 #define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
 #define UFC_OPT_SEAL_KERNEL 3    /* fixed-stride seals: */
 #define UFC_SEAL_INLINE 0        /*   the CRC kernel writes each workgroup's trailers after its reads (default) */

@@ -103,13 +103,11 @@ def varlen(eng, dev, reps, n=10_000_000):
     med, mean = timed(fn, reps)
     ceil_gbs = ceiling(eng, data, reps)
     algo = total + 8 * (n + 1) + 4 * n + n
-    # A/B: the other variable-length kernel on the same batch (sorted-runs 8-lane sets vs byte streams)
+    # A/B: the generic kernel on the same batch (the same results, timed beside the product kernel)
     from uflow_amd import _native as N
-    other = N.UFC_VARLEN_SORTED8 if eng.get_option(N.UFC_OPT_VARLEN_KERNEL) in (N.UFC_VARLEN_STREAM,) else N.UFC_VARLEN_STREAM
+    other = N.UFC_VARLEN_GENERIC
     saved = eng.get_option(N.UFC_OPT_VARLEN_KERNEL)
-    if N.lib().ufc_ctx_set_option(eng._ctx, N.UFC_OPT_VARLEN_KERNEL, other) != N.UFC_OK:
-        other = N.UFC_VARLEN_GENERIC  # (the streaming kernel: tuning builds only)
-        eng.set_option(N.UFC_OPT_VARLEN_KERNEL, other)
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, other)
     crc2 = torch.empty(n, dtype=torch.int32, device=dev)
     valid2 = torch.empty(n, dtype=torch.uint8, device=dev)
     fn2 = lambda: eng.crc_varlen(data, offsets, crc_out=crc2, valid_out=valid2)  # noqa: E731
@@ -119,7 +117,7 @@ def varlen(eng, dev, reps, n=10_000_000):
     settle(fn2)
     med2, _ = timed(fn2, reps)
     eng.set_option(N.UFC_OPT_VARLEN_KERNEL, saved)
-    ab = {"other_kernel": {N.UFC_VARLEN_STREAM: "stream", N.UFC_VARLEN_SORTED8: "sorted8"}.get(other, "generic"),
+    ab = {"other_kernel": "generic",
           "other_kernel_ms": round(med2, 4),
           "other_equal_results": same}
     if not CHECK:
@@ -272,7 +270,7 @@ def host(eng, reps=5, n=1_000_000, L=1472):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--varlen-kernel", default="auto", choices=["auto", "sorted8", "stream"],
+    ap.add_argument("--varlen-kernel", default="auto", choices=["auto", "sorted8"],
                     help="variable-length kernel of the timed runs (the other one is timed beside it)")
     ap.add_argument("--only", default="varlen,shard,seal,seal_varlen,parse,host")
     ap.add_argument("--reps", type=int, default=20)
@@ -284,8 +282,7 @@ def main():
     dev = torch.device("cuda", 0)
     eng = FrameCrcEngine(0)
     from uflow_amd import _native as N
-    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, {"auto": N.UFC_VARLEN_AUTO, "sorted8": N.UFC_VARLEN_SORTED8,
-                                             "stream": N.UFC_VARLEN_STREAM}[a.varlen_kernel])
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, {"auto": N.UFC_VARLEN_AUTO, "sorted8": N.UFC_VARLEN_SORTED8}[a.varlen_kernel])
     for what in a.only.split(","):
         if what == "host":
             for r in host(eng):

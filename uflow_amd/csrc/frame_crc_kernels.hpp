@@ -69,11 +69,6 @@ const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int 
 // {start (u64), len (u32), index in the run (bits 0..5) | past-the-end (bit 31)}.
 constexpr int kRunFrames = 64;
 int sort_runs(const uint64_t* offsets, bool pairs, uint64_t nframes, void* records, void* stream);
-// Sorted block-stream variable-length kernel (frame_crc_varlen2.hip): one 1024-thread workgroup per
-// CU, frames of 4..1532 B on the fast path.  pairs: (start, end) pairs with bytes_len < 2^31 - 1024.
-// Seal + pairs is not instantiated (nullptr).
-constexpr int kVarlen2Threads = 1024;
-const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // Sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): 8-frame sets from the
 // run-sorted records (p.offsets = records, p.offsets_csr = the CSR offsets or nullptr for pairs),
 // A^128 chain tables and the 32-slot nibble image; 12 waves, 2 sets in flight per wave.  insort:
@@ -82,11 +77,6 @@ const void* varlen2_kernel_symbol(bool seal, bool pairs);
 // 2^31 - 2^20 bytes (32-bit offsets from the buffer).
 // geor: each run's geometry computed once per frame before the sort (GEOR in frame_crc_varlen8.hip).
 const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw = 64, int aux = 0, bool geor = false);
-// Byte-balanced streaming kernel (frame_crc_varlen8.hip): CSR batches, 12 waves per workgroup, one
-// workgroup per CU; tables as the 8-lane kernel (A^128 chains, the 32-slot nibble image).  A launch
-// covers fewer than 2^31 frames.
-constexpr int kStreamWaves = 12;
-const void* stream8_kernel_symbol(bool seal);
 // Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride
 // + lens[i] (ufc_validate_host_slots_async).
 int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream);

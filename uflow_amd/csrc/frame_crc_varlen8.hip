@@ -681,390 +681,6 @@ UFC_V8_INSTW(true, 32) UFC_V8_INSTA(8) UFC_V8_INSTA(16) UFC_V8_INSTA(32) UFC_V8_
 #undef UFC_V8_INSTA
 #undef UFC_V8_INSTG
 
-// =============================================================================================
-// Byte-balanced streaming kernel (round 3, SURVEY.md section 7 step 6: "one byte stream"): CSR
-// batches only.  The batch's bytes [offsets[0], offsets[n]) are split into equal byte ranges, one per
-// 8-lane group of the grid (a binary search of the range start in the offsets gives the group's first
-// frame); a group walks the frames that START in its range in order, one 128-byte piece per step:
-// every frame's window is right-aligned as in the set kernel above (window end = the frame's end
-// rounded up to 4 bytes, so the trailer and the slot constants sit at fixed positions), consecutive
-// frames' windows follow each other through memory, and the piece two frames share is read twice in a
-// row (an L1/L2 hit, not a second HBM read).  So a wave-instruction reads 8 groups x 128 contiguous
-// bytes of 8 byte streams, with no per-set idle lanes (no max block count) and no sorting.
-//   * Geometry of 8 frames at a time per group (one frame per lane, two windows: current + next),
-//     a load cursor DEPTH pieces ahead of the compute cursor; each ring slot carries its piece's
-//     packed info (pad, t, first/last, live, ...) to the compute side.
-//   * Frame ends come at different steps in different groups: a finished frame's chains wait in a
-//     one-frame pending slot per group, and the finish (32 nibble products + DPP + A^-t, the same as
-//     group_lin8) runs for all groups at once when every group has a pending frame or one must push
-//     a second: about one finish round per four steps instead of one whenever any group ends.
-//   * Frames the fast path cannot take (shorter than 4 bytes, ending past offsets[n] after rounding,
-//     windows starting before the buffer or 2 GB past the wave's base, longer than 32 MB) run
-//     byte-wise in the same loop.
-#ifdef UFC_TUNING
-namespace {
-
-constexpr uint32_t kStrOob = 0x80000000u;
-constexpr uint32_t kStrLimit = 0x7FF00000u;  // window ends relative to the wave's base stay below
-constexpr uint64_t kStrMaxLen = 1ull << 25;  // fast path: frames up to 32 MB (19-bit piece counts)
-// Frame geometry (one VGPR): pad [0,8), t [8,10), len >= 5 [10], slow [11], end [12], P [13,32).
-__device__ __forceinline__ uint32_t sg_pad(uint32_t g) { return g & 255u; }
-__device__ __forceinline__ uint32_t sg_t(uint32_t g) { return (g >> 8) & 3u; }
-__device__ __forceinline__ uint32_t sg_P(uint32_t g) { return g >> 13; }
-constexpr uint32_t kSgLen5 = 1u << 10, kSgSlow = 1u << 11, kSgEnd = 1u << 12;
-// Ring-slot info (one VGPR): pad [0,8), t [8,10), first [10], last [11], len >= 5 [12], live [13],
-// slow marker [14], g1 (piece 1 of a frame whose G reaches into it) [15].
-constexpr uint32_t kRiFirst = 1u << 10, kRiLast = 1u << 11, kRiLen5 = 1u << 12, kRiLive = 1u << 13,
-                   kRiSlow = 1u << 14, kRiG1 = 1u << 15;
-
-__device__ __forceinline__ uint64_t mul_div64(uint64_t a, uint64_t b, uint64_t c) {
-  return (uint64_t)((unsigned __int128)a * b / c);
-}
-
-}  // namespace
-
-template <bool SEAL, int WAVES>
-__global__ __launch_bounds__(WAVES * 64) void frame_crc_stream8_kernel(const KernelParams p) {
-  constexpr int NS = 5;  // ring slots: NS - 1 pieces in flight while one is computed
-  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-  Lane8 L;
-  init_lane8(L, lds, p.G);
-  const uint32_t c = L.col, g = L.grp;
-  const uint64_t n = p.nframes;
-  const uint64_t* off = p.offsets;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
-
-  // ---- this group's byte range and first frame ----
-  const uint64_t off0 = *as_global<g_u64>(off), offn = *as_global<g_u64>(off + n);
-  const uint64_t B = offn >= off0 ? offn - off0 : 0;
-  const uint64_t NG = (uint64_t)gridDim.x * WAVES * 8;
-  const uint64_t gw = ((uint64_t)blockIdx.x * WAVES + wid) * 8;  // the wave's first group
-  const uint64_t gi = gw + g;
-  const uint64_t U_lo = off0 + mul_div64(B, gi, NG);
-  const uint64_t U_hi = gi + 1 == NG ? ~0ull : off0 + mul_div64(B, gi + 1, NG);
-  // base of the wave's buffer resource: below every window of its groups (pads <= 131 B)
-  const uint64_t U_w = off0 + mul_div64(B, gw, NG);
-  const uint64_t wbase = (U_w >= 256 ? U_w - 256 : 0) & ~3ull;
-  // first frame f with off[f] >= U_lo: 8-ary search by the group's 8 lanes, [lo, hi] holds the answer
-  uint64_t lo = 0, hi = n;
-  while (__builtin_amdgcn_ballot_w64(hi > lo) != 0) {
-    const uint64_t span = hi - lo;
-    const uint64_t m = lo + span * (c + 1) / 9;
-    const bool ge = hi > lo && *as_global<g_u64>(off + (m < n ? m : n)) >= U_lo;
-    const uint32_t msk = (uint32_t)(__builtin_amdgcn_ballot_w64(ge) >> (8 * g)) & 0xFFu;
-    if (hi > lo) {
-      if (msk == 0) {
-        lo = lo + span * 8 / 9 + 1;
-      } else {
-        const uint32_t k = (uint32_t)__builtin_ctz(msk);
-        hi = lo + span * (k + 1) / 9;
-        lo = k == 0 ? lo : lo + span * k / 9 + 1;
-      }
-    }
-  }
-  const uint64_t f_lo = lo;
-
-  // ---- frame geometry, 8 frames per group window (lane c: frame wfb + c) ----
-  const uint32_t baddr = (uint32_t)(uintptr_t)p.bytes;
-  auto geo_of = [&](uint64_t f, uint64_t S, uint64_t E, uint32_t& wend) -> uint32_t {
-    if (f >= n || S >= U_hi) return kSgEnd;
-    const uint64_t len = E >= S ? E - S : 0;
-    const uint32_t t = (0u - (baddr + (uint32_t)E)) & 3u;
-    const uint64_t P = (len + t + 4 + 127) >> 7;
-    const uint32_t pad = (uint32_t)(P * 128 - len - t);
-    const uint64_t wend64 = E + t - wbase;
-    // (a window starting before the buffer: its lane that straddles byte 0 would load nothing)
-    const bool slow = len < 4 || len > kStrMaxLen || E + t > offn || wend64 >= kStrLimit || S < (uint64_t)pad;
-    wend = slow ? 0u : (uint32_t)wend64;
-    return slow ? (kSgSlow | (len >= 5 ? kSgLen5 : 0u))
-                : (pad | (t << 8) | (len >= 5 ? kSgLen5 : 0u) | ((uint32_t)P << 13));
-  };
-  auto raw_load = [&](uint64_t fb, uint64_t& S, uint64_t& E) {
-    const uint64_t f = fb + c;
-    S = *as_global<g_u64>(off + (f < n ? f : n));
-    E = *as_global<g_u64>(off + (f + 1 < n ? f + 1 : n));
-  };
-  uint64_t wfb = f_lo;  // first frame of window A (group-uniform)
-  uint32_t GA, GB, WA, WB;
-  uint64_t RS, RE;  // raw offsets of the window after B (loaded one window ahead)
-  {
-    uint64_t S0, E0, S1, E1;
-    raw_load(wfb, S0, E0);
-    raw_load(wfb + 8, S1, E1);
-    raw_load(wfb + 16, RS, RE);
-    GA = geo_of(wfb + c, S0, E0, WA);
-    GB = geo_of(wfb + 8 + c, S1, E1, WB);
-  }
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + wbase), 0, (int)kStrLimit, 0x00020000);
-
-  // load cursor (group-uniform): frame lf, piece lk of its lP pieces, geometry lg / window end lw
-  uint64_t lf = f_lo;
-  uint32_t lk = 0, lg = 0, lw = 0;
-  bool ldone = false;
-  auto take_geo = [&]() {  // geometry of frame lf from window A (lane lf - wfb of the group)
-    const int src = (int)((g * 8u + (uint32_t)(lf - wfb)) * 4u);
-    lg = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)GA);
-    lw = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)WA);
-    ldone = (lg & kSgEnd) != 0;
-    lk = 0;
-  };
-  take_geo();
-  auto next_frame = [&](bool adv) {
-    if (adv) lf++;
-    const bool shift = adv && lf - wfb == 8;
-    if (__builtin_amdgcn_ballot_w64(shift) != 0) {
-      if (shift) {  // window B becomes A; the raw offsets loaded a window ago become B
-        GA = GB;
-        WA = WB;
-        GB = geo_of(wfb + 16 + c, RS, RE, WB);
-        wfb += 8;
-        raw_load(wfb + 16, RS, RE);
-      }
-    }
-    if (__builtin_amdgcn_ballot_w64(adv) != 0) {  // (take_geo's bpermutes need every lane active)
-      const uint32_t pg = lg, pw = lw, pk = lk;
-      const bool pd = ldone;
-      take_geo();
-      lg = adv ? lg : pg;
-      lw = adv ? lw : pw;
-      lk = adv ? lk : pk;
-      ldone = adv ? ldone : pd;
-    }
-  };
-
-  // ring
-  uint4 X[NS];
-  uint32_t RI[NS], RA[NS];  // slot info, aux (fast: window end; slow: frame index)
-  // Issue the load of the load cursor's next piece into slot s.
-  auto issue = [&](int sl) {
-    uint32_t info = 0, aux = 0, voff = kStrOob;
-    bool adv = false;
-    if (!ldone) {
-      if (lg & kSgSlow) {
-        info = kRiLive | kRiSlow | (lg & kSgLen5 ? kRiLen5 : 0u);
-        aux = (uint32_t)lf;
-        adv = true;
-      } else {
-        const uint32_t P = sg_P(lg), pad = sg_pad(lg);
-        info = pad | (sg_t(lg) << 8) | (lk == 0 ? kRiFirst : 0u) | (lk + 1 == P ? kRiLast : 0u) |
-               (lg & kSgLen5 ? kRiLen5 : 0u) | kRiLive | ((lk == 1 && pad > 128u) ? kRiG1 : 0u);
-        aux = lw;
-        voff = lw - 128u * (P - lk) + 16u * c;
-        if (lk == 0 && 16u * c + 20u <= pad) voff = kStrOob;  // lane wholly before the frame's G
-        lk++;
-        adv = lk == P;
-      }
-    }
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)voff, 0, 0);
-    X[sl] = make_uint4(v.x, v.y, v.z, v.w);
-    RI[sl] = info;
-    RA[sl] = aux;
-    next_frame(adv);
-  };
-
-  // compute state
-  Chains V{0u, 0u, 0u, 0u, 0u};
-  Chains PV{0u, 0u, 0u, 0u, 0u};  // pending frame's chains (tr: its trailer word, lane 7)
-  uint32_t pinfo = 0;              // pending: t [8,10), len >= 5 [12], valid pending [13]
-  uint64_t ptrail = 0;             // pending: the trailer's byte offset (seal)
-  uint64_t done_cnt = 0;           // frames finished by this group
-  uint32_t acc_crc = 0, acc_ok = 0;
-  auto store8 = [&](uint64_t first, uint32_t cnt) {  // results of frames first + c, c < cnt (hidden stores)
-    const uint64_t f = first + c;
-    if (c < cnt && f < n) {
-      if (p.crc_out) st_u32_hidden(p.crc_out + f, acc_crc);
-      if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_ok);
-    }
-  };
-  auto finish_round = [&]() {
-    const bool pend = (pinfo & kRiLive) != 0;
-    const uint32_t t = (pinfo >> 8) & 3u;
-    uint32_t lin = group_lin8(L, PV);
-    if (__builtin_amdgcn_ballot_w64(pend && t != 0) != 0) {
-      const uint32_t col = 40u + 3u * (L.grp & 3u) + (t ? t - 1u : 0u);
-      const uint32_t r = nib_mul<0>(L.lds, lin, col * 4u);
-      lin = t ? r : lin;
-    }
-    const uint32_t crc = ~lin;
-    const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)PV.tr);
-    const uint32_t ok = ((pinfo & kRiLen5) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
-    if (SEAL && pend && c == 7u && (pinfo & (1u << 16)))  // (len >= 4: the frame has a trailer)
-      st_u32_hidden((uint32_t*)(p.wbytes + ptrail), __builtin_bswap32(crc));
-    const uint32_t slot = (uint32_t)(done_cnt & 7u);
-    if (pend) {
-      acc_crc = c == slot ? crc : acc_crc;
-      acc_ok = c == slot ? ok : acc_ok;
-      done_cnt++;
-    }
-    const bool full = pend && slot == 7u;
-    if (__builtin_amdgcn_ballot_w64(full) != 0 && full) store8(f_lo + done_cnt - 8, 8u);
-    pinfo = 0;
-  };
-  auto sel_chains = [](bool cnd, Chains& dst, const Chains& src) {  // (field selects: no aggregate copy)
-    dst.v0 = cnd ? src.v0 : dst.v0;
-    dst.v1 = cnd ? src.v1 : dst.v1;
-    dst.v2 = cnd ? src.v2 : dst.v2;
-    dst.v3 = cnd ? src.v3 : dst.v3;
-    dst.tr = cnd ? src.tr : dst.tr;
-  };
-  auto push = [&](bool last, uint32_t info, uint64_t trail, bool has_trailer) {
-    if (__builtin_amdgcn_ballot_w64(last && (pinfo & kRiLive)) != 0) finish_round();
-    sel_chains(last, PV, V);
-    pinfo = last ? (info & ((3u << 8) | kRiLen5)) | kRiLive | (has_trailer ? (1u << 16) : 0u) : pinfo;
-    ptrail = last ? trail : ptrail;
-  };
-
-  // Byte path of the slow frames in this step (marker slots): lanes of the marker groups load the
-  // frame's words masked to it (any length), 128-byte pieces of a window that ends at the frame's end.
-  auto slow_frames = [&](bool mk, uint32_t fidx) {
-    uint64_t S = 0, E = 0;
-    if (mk) {
-      S = *as_global<g_u64>(off + fidx);
-      E = *as_global<g_u64>(off + fidx + 1);
-      E = E >= S ? E : S;
-    }
-    const uint64_t len = E - S;
-    const uint64_t n4 = len >= 4 ? len - 4 : len;
-    const uint64_t Ev = n4 + 4;                      // virtual end (a zero trailer when len < 4)
-    const uint64_t P = mk ? (Ev + 4 + 127) >> 7 : 0;  // pieces of the window [.. G | frame | T]
-    const uint32_t pad = (uint32_t)(P * 128 - Ev);
-    uint64_t pmax = 0;
-#pragma unroll
-    for (int q = 0; q < 8; q++) pmax = max(pmax, (uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)P, 8 * q));
-    const uintptr_t f0 = (uintptr_t)p.bytes + (uintptr_t)S, f1 = f0 + len;
-    auto piece = [&](int64_t o) -> uint4 {  // frame bytes [o, o + 16), zeros outside the frame
-      const uintptr_t Pa = f0 + (intptr_t)o, A = Pa & ~(uintptr_t)3;
-      const uint32_t sh = (uint32_t)(Pa & 3u);
-      uint32_t w[5];
-#pragma unroll
-      for (int k = 0; k < 5; k++) {
-        const uintptr_t ak = A + 4 * k;
-        w[k] = (mk && ak < f1 && ak + 4 > f0) ? *as_global<g_u32>((const uint32_t*)ak) : 0u;
-      }
-      uint32_t x[4];
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int64_t ob = o + 4 * i;
-        const uint32_t lo = (uint32_t)min(max(-ob, (int64_t)0), (int64_t)4);
-        const uint32_t hi = (uint32_t)min(max((int64_t)len - ob, (int64_t)0), (int64_t)4);
-        const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u), mlo = lo >= 4u ? 0u : (~0u << (8u * lo));
-        x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh) & mhi & mlo;
-      }
-      return make_uint4(x[0], x[1], x[2], x[3]);
-    };
-    Chains cs{0u, 0u, 0u, 0u, 0u};
-#pragma unroll 1
-    for (uint64_t k = 0; k < pmax; k++) {
-      const int64_t o = (int64_t)(128 * k + 16 * c) - (int64_t)pad;
-      uint4 x = piece(o);
-      const bool act = k < P;
-      if (k + 1 == P && c == 7u) {  // trailer (zeros when len < 4: beyond the frame)
-        cs.tr = x.w;
-        x.w = 0u;
-      }
-      if (k == 0) {
-        const uint4 fx = fix_piece(L.lds, x, (int)pad - (int)(16u * c));
-        cs.v0 = act ? fx.x : cs.v0;
-        cs.v1 = act ? fx.y : cs.v1;
-        cs.v2 = act ? fx.z : cs.v2;
-        cs.v3 = act ? fx.w : cs.v3;
-      } else {
-        if (k == 1) x = fix_piece(L.lds, x, (int)pad - 128 - (int)(16u * c));
-        Chains nc = cs;
-        chain4(L, nc, x);
-        sel_chains(act, cs, nc);
-      }
-    }
-    // as a fast frame's pending entry (t = 0: the window ends at the frame's end)
-    sel_chains(mk, V, cs);
-    push(mk, mk && len >= 5 ? kRiLen5 : 0u, S + n4, mk && len >= 4);
-  };
-
-  // One step on slot sl: issue the next piece into slot (sl + NS - 1) % NS, then compute slot sl.
-  auto step = [&](int sl, int fill) {
-    issue(fill);
-    __builtin_amdgcn_sched_barrier(0);
-    const uint32_t info = RI[sl];
-    uint4 x = X[sl];
-    const bool live = (info & kRiLive) != 0;
-    const bool mk = live && (info & kRiSlow);
-    if (__builtin_amdgcn_ballot_w64(mk) != 0) slow_frames(mk, RA[sl]);
-    const bool fast = live && !mk;
-    const bool first = fast && (info & kRiFirst), last = fast && (info & kRiLast);
-    const uint32_t pad = info & 255u, t = (info >> 8) & 3u;
-    if (last && c == 7u) {  // trailer = the 4 bytes before the window's last t; CRC'd as zeros
-      V.tr = t ? __builtin_amdgcn_alignbyte(x.w, x.z, 4u - t) : x.w;
-      x.z &= 0xFFFFFFFFu >> (8u * t);
-      x.w = 0u;
-    }
-    uint4 fx = x;
-    if (__builtin_amdgcn_ballot_w64(first) != 0) fx = fix_piece(L.lds, x, (int)pad - (int)(16u * c));
-    if (__builtin_amdgcn_ballot_w64(fast && (info & kRiG1)) != 0 && (info & kRiG1))
-      x = fix_piece(L.lds, x, (int)pad - 128 - (int)(16u * c));
-    Chains nv = V;
-#if defined(UFC_TUNING) && defined(UFC_STR_ABL) && (UFC_STR_ABL & 1)  // A/B: loads + control only
-    nv.v0 ^= x.x; nv.v1 ^= x.y; nv.v2 ^= x.z; nv.v3 ^= x.w;
-#else
-    chain4(L, nv, x);
-#endif
-    if (fast) {
-      V.v0 = first ? fx.x : nv.v0;
-      V.v1 = first ? fx.y : nv.v1;
-      V.v2 = first ? fx.z : nv.v2;
-      V.v3 = first ? fx.w : nv.v3;
-    }
-    push(last, info, wbase + (uint64_t)RA[sl] - t - 4u, true);
-    // every group has a frame waiting: one finish round for all of them
-    if (__builtin_amdgcn_ballot_w64(!(pinfo & kRiLive)) == 0) finish_round();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  // prologue: NS - 1 pieces in flight before the tables are staged
-#pragma unroll
-  for (int i = 0; i < NS - 1; i++) issue(i);
-  stage_store<WAVES * 64>(sr, lds);
-  fixtab_store(lds, p.G);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-
-  // rounds of NS steps while anything is to be loaded or in flight (a frame still pending when
-  // every stream is drained is finished after the loop: nothing inside it would finish it)
-  auto busy = [&]() -> bool {
-    bool b = !ldone;
-#pragma unroll
-    for (int i = 0; i < NS; i++) b = b || (RI[i] & kRiLive);
-    return __builtin_amdgcn_ballot_w64(b) != 0;
-  };
-  while (busy()) {
-    step(0, 4);
-    step(1, 0);
-    step(2, 1);
-    step(3, 2);
-    step(4, 3);
-  }
-  if (__builtin_amdgcn_ballot_w64(pinfo & kRiLive) != 0) finish_round();
-  const uint32_t rem = (uint32_t)(done_cnt & 7u);
-  if (rem) store8(f_lo + done_cnt - rem, rem);
-}
-
-// Measured slower than the 8-lane set kernel on config 3 (2.82 against 1.55 ms, the same box; its
-// loads + control alone, without the CRC steps, take 2.39 ms: DESIGN.md section 5.2): tuning builds only.
-#define UFC_STR_INST(SEAL) template __global__ void frame_crc_stream8_kernel<SEAL, 12>(const KernelParams);
-UFC_STR_INST(false) UFC_STR_INST(true)
-#undef UFC_STR_INST
-#endif
-
-const void* stream8_kernel_symbol(bool seal) {
-#ifdef UFC_TUNING
-  return seal ? (const void*)frame_crc_stream8_kernel<true, 12> : (const void*)frame_crc_stream8_kernel<false, 12>;
-#else
-  (void)seal;
-  return nullptr;
-#endif
-}
-
 const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux, bool geor) {
   if (geor) {
     if (!insort || sortw != 64 || aux != kV8Aux) return nullptr;

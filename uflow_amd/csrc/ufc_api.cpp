@@ -294,39 +294,6 @@ int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipSt
 }
 #endif  // UFC_TUNING
 
-// The sorted block-stream kernel (frame_crc_varlen2.hip, UFC_VARLEN_BLOCKSTREAM), CSR batches and pairs.
-// Pairs need the buffer below 2^31 - 1024 bytes (32-bit relative offsets); seal + pairs is not an
-// entry point.  Returns UFC_ERR_INVALID_ARG when the kernel does not apply (the caller falls back).
-#ifdef UFC_TUNING
-int launch_varlen2(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  const void* fn = ufc_dev::varlen2_kernel_symbol(seal, pairs);
-  if (!fn || (pairs && kp.frame_len >= ((uint64_t)1 << 31) - 1024)) return UFC_ERR_INVALID_ARG;
-  kp.chain_tab = ctx->d_chain;
-  kp.nib_img = ctx->d_nib;
-  kp.G = ctx->G;
-  // Launches of < 2^31 frames (32-bit per-wave frame counts, 6-bit window indices); offsets stay
-  // absolute (relative to kp.bytes), a launch only shifts the offsets and output pointers.
-  const uint64_t chunk = (uint64_t)1 << 31;
-  const uint64_t total = kp.nframes;
-  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
-    ufc_dev::KernelParams c = kp;
-    c.nframes = std::min(chunk, total - f0);
-    c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
-    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
-    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
-    // one workgroup (16 waves) per CU; at least ~64 frames per wave
-    const uint64_t waves = ufc_dev::kVarlen2Threads / 64;
-    uint64_t blocks = (c.nframes + 64 * waves - 1) / (64 * waves);
-    if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
-    if (blocks < 1) blocks = 1;
-    void* args[] = {&c};
-    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3(ufc_dev::kVarlen2Threads), args, 0, stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-  }
-  return UFC_OK;
-}
-#endif  // UFC_TUNING
-
 // The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): one launch per chunk of
 // < 2^29 frames, each run of 64 frames sorted by block count inside the kernel (tuning builds: the
 // sort_runs pre-pass into per-stream scratch instead, UFC_V8_PRESORT=1).  Any
@@ -399,31 +366,6 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
   return UFC_OK;
 }
 
-// The byte-balanced streaming kernel (frame_crc_varlen8.hip, frame_crc_stream8_kernel): CSR batches,
-// one launch per chunk of < 2^29 frames (offsets stay absolute; a chunk shifts the offsets and outputs).
-int launch_stream8(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  const void* fn = ufc_dev::stream8_kernel_symbol(seal);
-  if (!fn) return UFC_ERR_INVALID_ARG;
-  kp.chain_tab = ctx->d_chain128;
-  kp.nib_img = ctx->d_nib32;
-  kp.G = ctx->G;
-  const uint64_t chunk = (uint64_t)1 << 29;
-  const uint64_t total = kp.nframes;
-  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
-    ufc_dev::KernelParams c = kp;
-    c.nframes = std::min(chunk, total - f0);
-    c.offsets = kp.offsets + f0;
-    c.offsets_csr = c.offsets;
-    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
-    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
-    void* args[] = {&c};
-    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)ctx->ncu), dim3((unsigned)(ufc_dev::kStreamWaves * 64)),
-                                         args, 0, stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-  }
-  return UFC_OK;
-}
-
 // Variable-length batches: the sorted-runs kernel by default; the claimed 16-wave and blocked 8-wave
 // schedules, the block-stream kernel and the generic kernel by option.
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream);
@@ -447,17 +389,10 @@ Config varlen_config(const ufc_ctx* ctx) {
 
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
   const int opt = ctx->opt[UFC_OPT_VARLEN_KERNEL];
-  if (opt == UFC_VARLEN_STREAM && !pairs) return launch_stream8(ctx, seal, kp, stream);
-  if (opt == UFC_VARLEN_SORTED8 || opt == UFC_VARLEN_AUTO || opt == UFC_VARLEN_STREAM) {
+  if (opt == UFC_VARLEN_SORTED8 || opt == UFC_VARLEN_AUTO) {
     const int rc = launch_varlen8(ctx, seal, pairs, kp, stream);
     if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the 4-lane kernel below)
   }
-#ifdef UFC_TUNING
-  if (opt == UFC_VARLEN_BLOCKSTREAM) {
-    const int rc = launch_varlen2(ctx, seal, pairs, kp, stream);
-    if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the round-1 kernel below)
-  }
-#endif
   if (opt == UFC_VARLEN_GENERIC && !pairs)
     return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen | (seal ? ufc_dev::kModeSeal : 0), kp, stream);
 #ifdef UFC_TUNING
@@ -534,6 +469,7 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
       break;
     case UFC_OPT_VARLEN_KERNEL:
       if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_STREAM) return UFC_ERR_INVALID_ARG;
+      if (value == UFC_VARLEN_BLOCKSTREAM || value == UFC_VARLEN_STREAM) return UFC_ERR_INVALID_ARG;  // (removed)
 #ifndef UFC_TUNING
       if (value != UFC_VARLEN_AUTO && value != UFC_VARLEN_GENERIC && value != UFC_VARLEN_SORTED8)
         return UFC_ERR_INVALID_ARG;  // (round-1 and block-stream kernels: A/B in tuning builds)
@@ -602,7 +538,6 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
                                       : std::strcmp(k, "sorted") == 0 ? UFC_VARLEN_SORTED
                                       : std::strcmp(k, "blocked8") == 0 ? UFC_VARLEN_BLOCKED8
                                       : std::strcmp(k, "claim16") == 0 ? UFC_VARLEN_CLAIM16
-                                      : std::strcmp(k, "blockstream") == 0 ? UFC_VARLEN_BLOCKSTREAM
                                       : std::strcmp(k, "sorted8") == 0 ? UFC_VARLEN_SORTED8 : UFC_VARLEN_AUTO;
   if (const char* j = std::getenv("UFC_FIXED_JC")) ctx->opt[UFC_OPT_GENERIC_JC] = std::atoi(j);
   if (const char* k = std::getenv("UFC_SEAL_KERNEL"))
