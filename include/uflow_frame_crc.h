@@ -119,8 +119,9 @@ int ufc_crc_batch_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, si
 /* Frame i occupies d_bytes[d_offsets[i] .. d_offsets[i+1]) (CSR, n+1 offsets, nondecreasing). */
 int ufc_crc_batch_varlen(ufc_ctx* ctx, const uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
                          uint32_t* d_crc_out, uint8_t* d_valid_out, void* stream);
-/* In-place seal of every frame (frame_len >= 4); d_crc_out nullable.  Fixed stride: two kernels
- * (the CRC words, then every trailer with non-temporal stores; UFC_OPT_SEAL_KERNEL). */
+/* In-place seal of every frame (frame_len >= 4); d_crc_out nullable.  Fixed stride: one kernel whose
+ * workgroups write their trailers after their reads (UFC_SEAL_INLINE, default), or two (the CRC words,
+ * then every trailer with non-temporal stores: UFC_SEAL_TWO_PASS); UFC_OPT_SEAL_KERNEL. */
 int ufc_seal_batch_fixed(ufc_ctx* ctx, uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,
                          uint32_t* d_crc_out, void* stream);
 int ufc_seal_batch_varlen(ufc_ctx* ctx, uint8_t* d_bytes, const uint64_t* d_offsets, size_t n,
