@@ -376,6 +376,55 @@ def test_parse_varlen_slow_paths_and_cap(engine):
     assert (got[cap:] == 0xA5).all()
 
 
+def test_parse_varlen_headers_at_span_ends(engine):
+    """Item headers that end right before the CRC trailer of a workgroup's last frame (frames
+    255, 511, ... and the batch's last): ack frames (the last group's 9 bytes, then the trailer) and
+    data frames whose last datagram has no payload, with frame lengths that put the span end at
+    every offset mod 4.  The emit's exact-offset 16-byte header load would run past the span there;
+    it takes the aligned pair instead.  Device parse vs the codec oracle, frame by frame."""
+    import random
+    from oracle import codec as C
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE
+    from test_codec_cpu import info_to_dict
+    rng = random.Random(77)
+    frames = []
+    for i in range(256 * 12):
+        if i % 2:
+            f = C.random_ack_frame(rng, 1 + i % 9)
+            if not f["frame_acks"]:
+                f["frame_acks"] = [{"base_id": 1, "bitfield": 2, "nonce": True}]
+        else:
+            f = C.random_data_frame(rng, 6)
+            dg = dict(sequence_id=rng.getrandbits(16), channel_id=rng.randrange(64),
+                      window_parent_lead=rng.getrandbits(16), channel_parent_lead=rng.getrandbits(16),
+                      fragment_id=3, fragment_id_last=9, data=b"")  # longest header, no payload
+            f["datagrams"] = list(f["datagrams"]) + [dg]
+        frames.append(C.frame_write(f))
+    offsets = np.zeros(len(frames) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum([len(f) for f in frames])
+    ends = {int(offsets[k]) % 4 for k in range(256, len(frames) + 1, 256)}
+    assert ends == {0, 1, 2, 3}, ends
+    data = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
+    for lead in (0, 1, 2, 3):  # the batch at every alignment of its base
+        buf = torch.zeros(lead + len(data), dtype=torch.uint8, device=DEV)
+        buf[lead:] = torch.from_numpy(data).to(DEV)
+        d = buf[lead:]
+        o = torch.from_numpy(offsets).to(DEV)
+        _, valid = engine.crc_varlen(d, o)
+        assert bool(valid.all())
+        infos, items, used = engine.parse_varlen(d, o, valid)
+        torch.cuda.synchronize()
+        infos = infos.cpu().numpy().view(FRAME_INFO_DTYPE).reshape(-1)
+        items = items.cpu().numpy().view(ITEM_DTYPE).reshape(-1)
+        total = 0
+        for i, fb in enumerate(frames):
+            assert infos[i]["ok"], i
+            cnt = int(infos[i]["item_count"])
+            assert info_to_dict(infos[i], items[total:total + cnt], fb) == C.frame_read(fb), (lead, i)
+            total += cnt
+        assert int(used.cpu()[0]) == total
+
+
 def test_parse_varlen_vs_host_parse_large(engine):
     """A 200k-frame batch: device parse == host parse (itself pinned to the oracle on CPU)."""
     from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host

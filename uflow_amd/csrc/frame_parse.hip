@@ -278,7 +278,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   }
 }
 
-template <int U, bool X4>
+template <int U, int X4>
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
     const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
@@ -328,8 +328,10 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
   const uint16_t* seg = pos_seg + (sb == 0xFFFFFFFFu ? 0u : sb);
   if (items) {
     // U items per thread per round (items g, g + 256, ...): every header load of the round is issued
-    // before the first decode and store.  X4: one 16-byte load + one dword per header instead of five
-    // dwords (a straddling dwordx4 is range-checked per dword).
+    // before the first decode and store.  X4 = 2: one unaligned 16-byte load at the header itself
+    // when all 16 bytes lie inside the workgroup's range (a header at the very end of the span takes
+    // the X4 = 1 pair, so no header byte depends on how a straddling load is range-checked); X4 = 1:
+    // an aligned 16-byte load + one dword; X4 = 0: five dwords.
     const uint64_t g_end = min((uint64_t)g1, cap);
     for (uint64_t gb = (uint64_t)g0 + t; gb < g_end; gb += (uint64_t)U * kParseThreads) {
       uint32_t hoff[U], fo[U], x[U][5];
@@ -362,8 +364,14 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
 #pragma unroll
         for (int u = 0; u < U; u++) {
           if (mm[u] == kItemsNone) continue;
-          const uint32_t al = ((uint32_t)(lstart[fo[u]] - span_lo) + delta + hoff[u]) & ~3u;
-          if constexpr (X4) {
+          const uint32_t ex = (uint32_t)(lstart[fo[u]] - span_lo) + delta + hoff[u];
+          const uint32_t al = ex & ~3u;
+          if (X4 == 2 && ex + 16 <= (uint32_t)range) {  // one unaligned 16-byte load at the header
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)ex, 0, 0);
+            x[u][0] = v.x, x[u][1] = v.y, x[u][2] = v.z, x[u][3] = v.w;
+            x[u][4] = 0;
+          } else if constexpr (X4 >= 1) {
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
             const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)al, 0, 0);
             x[u][0] = v.x, x[u][1] = v.y, x[u][2] = v.z, x[u][3] = v.w;
@@ -381,7 +389,8 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
         const uint32_t f = fo[u];
         uint32_t w[4];
         if (buf_ok) {
-          const uint32_t sh = ((uint32_t)(lstart[f] - span_lo) + delta + hoff[u]) & 3u;
+          const uint32_t ex = (uint32_t)(lstart[f] - span_lo) + delta + hoff[u];
+          const uint32_t sh = (X4 == 2 && ex + 16 <= (uint32_t)range) ? 0u : ex & 3u;
 #pragma unroll
           for (int q = 0; q < 4; q++) w[q] = __builtin_amdgcn_alignbyte(x[u][q + 1], x[u][q], sh);
         } else {
@@ -480,18 +489,20 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
   if (e != hipSuccess) return e;
-  // One item per thread per round, 16-byte header loads (0.526 against 0.551 ms with five dword loads;
-  // 4 items per round 0.532 with them, 0.543 without: DESIGN.md section 5.5).
-  auto emit = parse_emit_kernel<1, true>;
+  // One item per thread per round, one 16-byte load per header (0.526 against 0.551 ms with five
+  // dword loads; 4 items per round 0.532 with them, 0.543 without; the exact-offset load 0.453
+  // against 0.458 for the aligned pair: DESIGN.md section 5.5).
+  auto emit = parse_emit_kernel<1, 2>;
 #ifdef UFC_TUNING
-  {  // UFC_EMIT_U=1|2|4 items per thread per round, UFC_EMIT_X4=0: five dword loads per header
+  {  // UFC_EMIT_U=1|2|4 items per thread per round, UFC_EMIT_X4=0: five dword loads per header,
+     // 2: one unaligned 16-byte load at the header
     const char* wu = std::getenv("UFC_EMIT_U");
     const char* wx = std::getenv("UFC_EMIT_X4");
     const int eu = wu ? std::atoi(wu) : 1;
-    const bool x4 = !wx || std::atoi(wx) != 0;
-    if (eu == 2) emit = x4 ? parse_emit_kernel<2, true> : parse_emit_kernel<2, false>;
-    else if (eu == 4) emit = x4 ? parse_emit_kernel<4, true> : parse_emit_kernel<4, false>;
-    else if (!x4) emit = parse_emit_kernel<1, false>;
+    const int x4 = wx ? std::atoi(wx) : 2;
+    if (eu == 2) emit = x4 == 2 ? parse_emit_kernel<2, 2> : x4 ? parse_emit_kernel<2, 1> : parse_emit_kernel<2, 0>;
+    else if (eu == 4) emit = x4 == 2 ? parse_emit_kernel<4, 2> : x4 ? parse_emit_kernel<4, 1> : parse_emit_kernel<4, 0>;
+    else emit = x4 == 2 ? parse_emit_kernel<1, 2> : x4 ? parse_emit_kernel<1, 1> : parse_emit_kernel<1, 0>;
   }
 #endif
   emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
