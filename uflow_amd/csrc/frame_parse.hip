@@ -278,199 +278,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   }
 }
 
-// The walk with frames handed out on demand (tuning A/B, UFC_WALK_DYN=1).  One thread per frame
-// makes a workgroup last as long as its longest chain: a data frame of 63 datagrams is 63 dependent
-// header loads while an ack frame needs one read, so most lanes idle for most of the walk.  Here a
-// lane takes its next frame as soon as it is done with one.  Every lane is a small state machine
-// that issues at most one round of loads per loop iteration (a frame's first 16 bytes, or the next
-// datagram header), and idle lanes are handed frames from chunks of 64 that the wave claims from
-// the launch's counter one chunk ahead (their offsets and gate flags loaded when claimed, handed
-// to the lanes by ds_bpermute).  The header offsets go to a fixed 64-slot area per frame in
-// global memory (the emit reads them by frame index).  Frames shorter than 16 bytes and kinds whose
-// fields lie past byte 15 take the codec's byte reader in place.
-constexpr uint32_t kDynChunk = 64;
-enum : uint32_t { kDynIdle = 0, kDynHead = 1, kDynStep = 2, kDynDone = 3 };
-
-struct DevBytesHead16 {  // bytes 0..15 from two registers, the rest from global memory
-  const uint8_t* p;
-  uint64_t w0, w1;
-  __device__ uint32_t operator()(uint32_t i) const {
-    if (i < 8) return (uint32_t)(w0 >> (8 * i)) & 0xFFu;
-    if (i < 16) return (uint32_t)(w1 >> (8 * (i - 8))) & 0xFFu;
-    return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
-  }
-  __device__ uint32_t head3(uint32_t i) const { return *(g_u32_a1*)(p + i) & 0xFFFFFFu; }
-};
-struct NullSink {
-  static constexpr bool kDecode = false;
-  __device__ bool on() const { return false; }
-  __device__ void operator()(uint32_t, const ufc_item&) const {}
-  __device__ void header(uint32_t, uint32_t) const {}
-};
-
-__global__ __launch_bounds__(kParseThreads) void parse_walk_dyn_kernel(const uint8_t* bytes, const uint64_t* offsets,
-                                                                       uint64_t n, const uint8_t* valid,
-                                                                       ufc_frame_info* infos, uint32_t* counts,
-                                                                       uint8_t* modes, uint16_t* pos_frame,
-                                                                       unsigned long long* claim) {
-  const uint32_t lane = threadIdx.x & 63;
-  // A chunk: frames c .. c + m - 1 (m <= 64), lane j holding frame c + j's start, length and flag.
-  struct Chunk {
-    uint64_t c;
-    uint32_t m;
-    uint64_t a;
-    uint32_t len;
-    uint32_t v;
-  };
-  auto take = [&]() -> Chunk {
-    unsigned long long c0 = 0;
-    if (lane == 0) c0 = atomicAdd(claim, (unsigned long long)kDynChunk);
-    const uint64_t c = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(c0 >> 32)) << 32) |
-                       (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)c0);
-    Chunk k{c, c < n ? (uint32_t)min((uint64_t)kDynChunk, n - c) : 0u, 0, 0, 0};
-    if (lane < k.m) {
-      k.len = frame_len32(offsets, c + lane, k.a);
-      k.v = valid[c + lane];
-    }
-    return k;
-  };
-  Chunk A = take(), B = take();
-  uint32_t hA = 0;  // frames of A handed out
-  uint32_t st = kDynIdle;
-  uint64_t f = 0, a = 0;
-  uint32_t len = 0, v = 0, pos = 0, k = 0, cnt = 0, plen = 0, f0 = 0, aux = 0, h3 = 0;
-  uint64_t w0 = 0, w1 = 0;
-
-  auto finish = [&](const ufc_frame_info& info, bool ok, bool inline_data) {
-    const uint32_t c = ok ? info.item_count : 0u;
-    uint8_t mode = kItemsNone;
-    if (c) {
-      if (info.kind == UFC_FRAME_ACK)
-        mode = kItemsAck;
-      else
-        mode = (inline_data && c <= kPosSlots && len <= 0xFFFFu && pos_frame) ? kItemsPos : kItemsWalk;
-    }
-    ufc_frame_info o = info;
-    o.item_first = 0;  // written by the emit step
-    infos[f] = o;
-    counts[f] = c;
-    modes[f] = mode;
-    st = kDynIdle;
-  };
-  auto finish_data = [&](bool ok) {
-    ufc_frame_info info;
-    info.kind = UFC_FRAME_DATA;
-    info.ok = ok ? 1 : 0;
-    info.aux = (uint8_t)aux;
-    info.crc_ok = 1;
-    info.f[0] = f0;
-    info.f[1] = info.f[2] = info.f[3] = info.f[4] = 0;
-    info.item_count = ok ? cnt : 0u;
-    finish(info, ok, true);
-  };
-  // one datagram header (its first three bytes in h3) of the data frame at payload offset pos
-  auto step = [&]() {
-    uint32_t hs, dl;
-    ufc_codec::datagram_size([&](uint32_t c) -> uint32_t { return (h3 >> (8 * c)) & 0xFFu; }, hs, dl);
-    if (plen - pos < hs + dl) {
-      finish_data(false);
-      return;
-    }
-    if (k < kPosSlots && pos_frame) pos_frame[f * kPosSlots + k] = (uint16_t)(1 + pos);
-    pos += hs + dl;
-    k++;
-    if (k == cnt) {
-      finish_data(pos == plen);
-    } else if (plen - pos < 6) {
-      finish_data(false);
-    } else {
-      h3 = *(g_u32_a1*)(bytes + a + 1 + pos) & 0xFFFFFFu;  // (next iteration)
-      st = kDynStep;
-    }
-  };
-
-  while (true) {
-    if (st == kDynStep) {
-      step();
-    } else if (st == kDynHead) {
-      const uint32_t kind = (uint32_t)(w0 & 0xFFu);
-      if (v && kind == UFC_FRAME_DATA && len >= 10) {
-        plen = len - 5;
-        auto hb = [&](uint32_t i) -> uint32_t { return (uint32_t)(i < 8 ? w0 >> (8 * i) : w1 >> (8 * (i - 8))) & 0xFFu; };
-        f0 = (hb(1) << 24) | (hb(2) << 16) | (hb(3) << 8) | hb(4);
-        aux = hb(5) >> 7;
-        cnt = hb(5) & 0x7Fu;
-        pos = ufc_codec::kDataPayloadHeader;
-        k = 0;
-        if (cnt == 0) {
-          finish_data(pos == plen);
-        } else if (plen - pos < 6) {
-          finish_data(false);
-        } else {
-          h3 = hb(6) | (hb(7) << 8) | (hb(8) << 16);  // the first header is inside the 16 bytes
-          step();
-        }
-      } else {
-        ufc_frame_info info;
-        const bool ok = ufc_codec::read_frame_to(DevBytesHead16{bytes + a, w0, w1}, len, v != 0, info, NullSink{},
-                                                 kPosSlots);
-        finish(info, ok, false);
-      }
-    }
-    // hand frames to the idle lanes: A's rest first, then B (and B becomes A, a new B is claimed)
-    const uint64_t need = __builtin_amdgcn_ballot_w64(st == kDynIdle);
-    if (need) {
-      const uint32_t nneed = (uint32_t)__builtin_popcountll(need);
-      const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-      const uint32_t availA = A.m - hA;
-      const bool fromA = rank < availA;
-      const uint32_t j = fromA ? hA + rank : rank - availA;  // lane of the chunk holding the frame
-      const uint32_t jA = min(j, 63u) * 4, jB = min(j, 63u) * 4;
-      const uint32_t aA_lo = __builtin_amdgcn_ds_bpermute(jA, (int)(uint32_t)A.a);
-      const uint32_t aA_hi = __builtin_amdgcn_ds_bpermute(jA, (int)(uint32_t)(A.a >> 32));
-      const uint32_t lA = __builtin_amdgcn_ds_bpermute(jA, (int)A.len);
-      const uint32_t vA = __builtin_amdgcn_ds_bpermute(jA, (int)A.v);
-      uint32_t aB_lo = 0, aB_hi = 0, lB = 0, vB = 0;
-      if (nneed > availA) {  // (wave-uniform)
-        aB_lo = __builtin_amdgcn_ds_bpermute(jB, (int)(uint32_t)B.a);
-        aB_hi = __builtin_amdgcn_ds_bpermute(jB, (int)(uint32_t)(B.a >> 32));
-        lB = __builtin_amdgcn_ds_bpermute(jB, (int)B.len);
-        vB = __builtin_amdgcn_ds_bpermute(jB, (int)B.v);
-      }
-      if (st == kDynIdle) {
-        const bool has = fromA || j < B.m;
-        if (has) {
-          f = (fromA ? A.c : B.c) + j;
-          a = fromA ? (((uint64_t)aA_hi << 32) | aA_lo) : (((uint64_t)aB_hi << 32) | aB_lo);
-          len = fromA ? lA : lB;
-          v = fromA ? vA : vB;
-          if (len >= 16) {
-            w0 = *(g_u64_a1*)(bytes + a);  // (next iteration)
-            w1 = *(g_u64_a1*)(bytes + a + 8);
-            st = kDynHead;
-          } else {
-            ufc_frame_info info;
-            const bool ok = ufc_codec::read_frame_to(DevBytes{bytes + a}, len, v != 0, info, NullSink{}, kPosSlots);
-            finish(info, ok, false);  // (idle again: a frame next iteration)
-          }
-        } else {
-          st = B.m == 0 ? kDynDone : kDynIdle;  // (B empty: the counter is past n)
-        }
-      }
-      if (nneed > availA) {  // A used up: B becomes A, the next chunk is claimed
-        hA = min(nneed - availA, B.m);
-        A = B;
-        if (A.m) B = take();
-        else B.m = 0;
-      } else {
-        hA += nneed;
-      }
-    }
-    if (__builtin_amdgcn_ballot_w64(st != kDynDone) == 0) break;
-  }
-}
-
-template <int U, int X4, bool DYN = false>
+template <int U, int X4>
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
     const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
@@ -547,7 +355,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
           if (m == kItemsPos || m == kItemsAck) {
             mm[u] = m;
             fo[u] = f;
-            hoff[u] = m == kItemsPos ? (uint32_t)(DYN ? pos_seg[(i0 + f) * kPosSlots + k] : seg[lseg[f] + k])
+            hoff[u] = m == kItemsPos ? (uint32_t)seg[lseg[f] + k]
                                      : 1u + ufc_codec::kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
           }
         }
@@ -620,24 +428,15 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
 }  // namespace
 
 namespace {
-bool walk_dyn() {  // the walk with frames handed out on demand (tuning builds, UFC_WALK_DYN=1)
-#ifdef UFC_TUNING
-  const char* w = std::getenv("UFC_WALK_DYN");
-  return w && std::atoi(w) != 0;
-#else
-  return false;
-#endif
-}
 struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned parts)
   uint64_t counts, firsts, modes, cursor, bases, slots, temp, end, seg_cap;
-  ParseLayout(uint64_t n, uint64_t items_cap, size_t temp_bytes, bool dyn = walk_dyn()) {
+  ParseLayout(uint64_t n, uint64_t items_cap, size_t temp_bytes) {
     auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
     const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
     // u16 header slots; below 2^32 - 1 so that every segment fits 32-bit offsets and no segment base
     // can equal the overflow sentinel 0xFFFFFFFF (frames past the cap are walked again, kItemsWalk)
     seg_cap = std::min<uint64_t>(std::min<uint64_t>(n * kPosSlots, std::max<uint64_t>(items_cap, 1)),
                                  0xFFFFFFFEull - kSegWords);
-    if (dyn) seg_cap = items_cap ? n * kPosSlots : 0;  // (the dynamic walk: 64 slots per frame)
     counts = 0;
     firsts = counts + up(n * 4);
     modes = firsts + up(n * 4);
@@ -679,16 +478,7 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
 #ifdef UFC_TUNING
   if (const char* w = std::getenv("UFC_WALK_POOL")) pool = std::atoi(w) != 0;
 #endif
-  const bool dyn = walk_dyn();
-  uint64_t dyn_grid = 4096;  // workgroups of the dynamic walk (each takes chunks until the batch is out)
-#ifdef UFC_TUNING
-  if (const char* w = std::getenv("UFC_WALK_DYN_GRID")) dyn_grid = std::max(1, std::atoi(w));
-#endif
-  if (dyn)
-    parse_walk_dyn_kernel<<<(unsigned)std::min<uint64_t>(blocks, dyn_grid), kParseThreads, 0, stream>>>(
-        a.bytes, a.offsets, n, a.valid, a.infos, counts, modes,
-        (a.items && !std::getenv("UFC_WALK_DYN_NOSLOTS")) ? pos_seg : nullptr, cursor);
-  else if (pool)
+  if (pool)
     parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
                                                                            counts, modes, pos_seg, cursor, bases,
                                                                            lay.seg_cap);
@@ -713,7 +503,6 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
     if (eu == 2) emit = x4 == 2 ? parse_emit_kernel<2, 2> : x4 ? parse_emit_kernel<2, 1> : parse_emit_kernel<2, 0>;
     else if (eu == 4) emit = x4 == 2 ? parse_emit_kernel<4, 2> : x4 ? parse_emit_kernel<4, 1> : parse_emit_kernel<4, 0>;
     else emit = x4 == 2 ? parse_emit_kernel<1, 2> : x4 ? parse_emit_kernel<1, 1> : parse_emit_kernel<1, 0>;
-    if (dyn) emit = parse_emit_kernel<1, 2, true>;
   }
 #endif
   emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
