@@ -108,8 +108,8 @@ def test_seal_fixed(engine, seal_kernel):
                     if want_crc:
                         assert np.array_equal(crc_out.cpu().numpy().view(np.uint32), ref_crc)
                     assert ref_valid.all() or frame_len < 5
-    finally:
-        engine.set_option(N.UFC_OPT_SEAL_KERNEL, N.UFC_SEAL_TWO_PASS)
+    finally:  # back to the default (the one-kernel seal)
+        engine.set_option(N.UFC_OPT_SEAL_KERNEL, N.UFC_SEAL_INLINE)
 
 
 def _varlen_case(engine, rng, lens, seal=True, flip_every=0):
