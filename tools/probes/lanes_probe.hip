@@ -4,8 +4,10 @@
 // (4-frame sets, 256-byte pieces: the fixed kernel's layout), runs of 64 frames ordered by block
 // count (ballot ranks) or not, windows right-aligned to the frame end rounded up to 4 B, pieces wholly
 // before the frame out of range (no request), default cache policy, DEPTH sets in flight per wave, one
-// workgroup per CU.  Question: does the 16-lane layout's access pattern (3 lines per 256-B piece
-// instead of 2 per 128-B piece) stream faster?  Prints one line per variant (median of 9 launches).
+// workgroup per CU.  Question (round 4, first): does the 16-lane layout's access pattern (3 lines per
+// 256-B piece instead of 2 per 128-B piece) stream faster?  (Second, "full6"): what do the out-of-range
+// load instructions cost that the product kernel issues for the blocks past a set's own (it issues 6
+// blocks' loads for every set)?  Prints one line per variant (median of 9 launches).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,7 +19,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr uint32_t kOob = 0x80000000u;
 
 // LANES lanes per frame, 64 / LANES frames per set, piece = 16 * LANES bytes, JM blocks of 256 B max.
-template <int LANES, int D, int WAVES, bool SORT>
+template <int LANES, int D, int WAVES, bool SORT, bool FULL = false>
 __global__ __launch_bounds__(WAVES * 64) void vl(const uint8_t* bytes, const uint64_t* offsets, uint32_t nframes,
                                                  uint32_t* out) {
   __shared__ char pad_lds[160 * 1024];  // one workgroup per CU, as the kernels
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(WAVES * 64) void vl(const uint8_t* bytes, const uin
         Pg = __builtin_amdgcn_ds_bpermute((FPS * k + g) * 4, (int)s_P);
         uint32_t mx = 0;
         for (uint32_t q = 0; q < FPS; q++) mx = max(mx, (uint32_t)__builtin_amdgcn_readlane(s_P, FPS * k + q));
-        P = mx ? mx : 1;
+        P = FULL ? 6u * (256 / PIECE) : (mx ? mx : 1);  // FULL: every set issues 6 blocks' loads (out of range past its own)
       }
       const uint32_t wst = ws_g, front = fr_g;  // window start, bytes before the frame
       const uint32_t o = PIECE * j + 16 * c;
@@ -146,14 +148,17 @@ int main() {
   {"lanes=" #L_ " D=" #D_ " waves=" #W_ " sort=" #S_, [](const uint8_t* b, const uint64_t* o, uint32_t nn, uint32_t* ou) { \
      hipLaunchKernelGGL((vl<L_, D_, W_, S_>), dim3(256), dim3(W_ * 64), 0, 0, b, o, nn, ou);       \
    }}
+#define PVF(L_, D_, W_, S_)                                                                        \
+  {"lanes=" #L_ " D=" #D_ " waves=" #W_ " sort=" #S_ " full6", [](const uint8_t* b, const uint64_t* o, uint32_t nn, uint32_t* ou) { \
+     hipLaunchKernelGGL((vl<L_, D_, W_, S_, true>), dim3(256), dim3(W_ * 64), 0, 0, b, o, nn, ou); \
+   }}
   V vs[] = {{"stream", [](const uint8_t* b, const uint64_t* o, uint32_t nn, uint32_t* ou) {
                (void)o;
                (void)nn;
                hipLaunchKernelGGL(stream, dim3(256), dim3(512), 0, 0, b, g_total, ou);
              }},
-            PV(8, 4, 12, true),  PV(16, 4, 12, true), PV(16, 2, 12, true), PV(16, 4, 8, true),
-            PV(16, 6, 8, true),  PV(8, 4, 12, false), PV(16, 4, 12, false), PV(16, 6, 12, true),
-            PV(8, 12, 12, true), PV(16, 12, 12, true), PV(16, 12, 8, true), PV(8, 8, 12, true), PV(16, 8, 12, true)};
+            PV(8, 4, 12, true), PVF(8, 4, 12, true), PV(8, 8, 12, true), PVF(8, 8, 12, true), PV(8, 12, 12, true),
+            PVF(8, 12, 12, true)};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
