@@ -10,6 +10,8 @@ golden fixtures run straight through the HIP path.
              its CRC words must equal the GPU gate's.
   config 4   one GPU's shard of the 100M-frame batch: frames [37.5M, 50M) (rank 3 of 8) of seed
              0x5EED0003, 18.75 GB, sealed on the GPU, every 1000th frame flipped; as config 3.
+  parse      the parse workload of tools/bench_configs.py (1M uflow frames, 14.5M items), every
+             info and item vs the native host parse (itself pinned to the codec oracle on CPU).
 The oracle runs multithreaded over the whole batch (16 threads: the GPU box's CPU share).
 """
 import json
@@ -185,6 +187,43 @@ def test_golden_reference_frames_fixture(engine):
     d2, o2 = _csr(bad)
     _, v2 = _gpu_varlen(engine, d2, o2)
     assert not v2.any()
+
+
+def test_parse_bench_workload_full(engine):
+    """The parse workload tools/bench_configs.py times (1M uflow frames, 1.41 GB: data frames with
+    micro/small/large datagrams, receive-side data frames and ack frames, 600 distinct frames from the
+    codec oracle tiled), with one bit flipped in every 997th frame: the GPU gate + GPU parse vs the
+    native host parse with its own host gate (ufc_parse_batch_host, pinned to the codec oracle by the
+    CPU suite), every info and every item compared."""
+    import random
+    from oracle import codec as C
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host
+    n = 1_000_000
+    rng = random.Random(5)
+    base = [C.frame_write(C.random_data_frame(rng) if i % 3 == 0 else C.receive_side_data_frame(rng)
+                          if i % 3 == 1 else C.random_ack_frame(rng, 20)) for i in range(600)]
+    lens = np.array([len(base[i % 600]) for i in range(n)], dtype=np.int64)
+    offsets = np.zeros(n + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    blob = np.frombuffer(b"".join(base), dtype=np.uint8)
+    data = np.concatenate([blob] * (n // 600 + 1))[: int(offsets[-1])].copy()
+    flipped = np.arange(0, n, 997)
+    data[offsets[flipped] + (lens[flipped] // 2)] ^= 0x10
+    d = torch.from_numpy(data).to(DEV)
+    o = torch.from_numpy(offsets).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    k = int(used.cpu()[0])
+    got_infos = _host(infos).view(FRAME_INFO_DTYPE).reshape(-1)
+    got_items = _host(items[:k]).view(ITEM_DTYPE).reshape(-1)
+    ref_infos, ref_items = parse_batch_host(data, offsets.astype(np.uint64), None, nthreads=THREADS)
+    assert int(got_infos["crc_ok"].sum()) == n - flipped.size
+    assert k == ref_items.size and k > 14_000_000, k
+    bad = np.nonzero((got_infos.view(np.uint8).reshape(n, -1) != ref_infos.view(np.uint8).reshape(n, -1)).any(1))[0]
+    assert bad.size == 0, f"{bad.size} frame infos differ, first frames {bad[:8]}"
+    bad = np.nonzero((got_items.view(np.uint8).reshape(k, -1) != ref_items.view(np.uint8).reshape(k, -1)).any(1))[0]
+    assert bad.size == 0, f"{bad.size} items differ, first items {bad[:8]}"
 
 
 def test_parse_datagram_validity_flags(engine):
