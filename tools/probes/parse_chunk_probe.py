@@ -4,8 +4,8 @@ MI355X's 256-MB Infinity Cache?  (tuning probe for frame_parse.hip, DESIGN.md se
 The walk reads every item header's line and the emit reads the same lines again; over the whole 1M-frame
 batch (1.41 GB) the walk's lines have left every cache before the emit reaches them.  This times the
 bench's parse workload (tools/bench_configs.py `parse`) as one call and as consecutive calls over chunks
-of C frames on one stream (each chunk's walk, scan and emit back to back; item bases from a first full
-parse), and checks that the chunked items equal the whole-batch items.  Prints one JSON line per C and
+of C frames on one stream or spread over 2-4 streams (each chunk's walk, scan and emit back to back on
+its stream, so one chunk's walk can run beside another's emit; item bases from a first full parse), and checks that the chunked items equal the whole-batch items.  Prints one JSON line per C and
 exits non-zero if any chunked result differs.  Run on the GPU box: python tools/probes/parse_chunk_probe.py
 """
 import ctypes
@@ -45,13 +45,21 @@ def main():
     item_first = fi["item_first"].astype(np.int64)
     ref_items = items[:total].clone()
     lib = N.lib()
-    stream = torch.cuda.current_stream().cuda_stream
     out_items = torch.empty_like(items)
     out_infos = torch.empty_like(infos)
     used_k = torch.zeros(1, dtype=torch.int64, device="cuda")
 
-    def run(chunk):
-        for c0 in range(0, n, chunk):
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()]
+    ev_done = [torch.cuda.Event() for _ in streams]
+
+    def run(chunk, ns=1):
+        if ns > 1:  # chunk c on stream c % ns, all forked from and joined back into the current stream
+            ev_start = torch.cuda.Event()
+            ev_start.record(streams[0])
+            for s in streams[1:ns]:
+                s.wait_event(ev_start)
+        for ci, c0 in enumerate(range(0, n, chunk)):
+            st = streams[ci % ns].cuda_stream
             nk = min(chunk, n - c0)
             b = int(item_first[c0])
             e = int(item_first[c0 + nk]) if c0 + nk < n else total
@@ -60,9 +68,12 @@ def main():
                                             ctypes.c_void_p(valid.data_ptr() + c0),
                                             ctypes.c_void_p(out_infos.data_ptr() + 32 * c0),
                                             ctypes.c_void_p(out_items.data_ptr() + 24 * b), max(e - b, 1),
-                                            ctypes.c_void_p(used_k.data_ptr()), ctypes.c_void_p(stream))
+                                            ctypes.c_void_p(used_k.data_ptr()), ctypes.c_void_p(st))
             if rc != 0:
                 raise RuntimeError(f"parse rc {rc}")
+        for i in range(1, ns):
+            ev_done[i].record(streams[i])
+            streams[0].wait_event(ev_done[i])
 
     # settle: clocks ramp up from idle over ~1 s
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -75,21 +86,21 @@ def main():
             break
     bad = 0
     for rnd in range(2):
-        for chunk in (n, 500_000, 250_000, 125_000, 62_500, 31_250):
+        for chunk, ns in ((n, 1), (500_000, 1), (500_000, 2), (250_000, 2), (250_000, 4), (125_000, 4)):
             out_items.fill_(0)
-            run(chunk)
+            run(chunk, ns)
             torch.cuda.synchronize()
             same = bool(torch.equal(out_items[:total], ref_items))
             bad += not same
             ts = []
             for _ in range(15):
                 ev0.record()
-                run(chunk)
+                run(chunk, ns)
                 ev1.record()
                 ev1.synchronize()
                 ts.append(ev0.elapsed_time(ev1))
             ts.sort()
-            print(json.dumps({"round": rnd, "chunk_frames": chunk, "calls": (n + chunk - 1) // chunk,
+            print(json.dumps({"round": rnd, "chunk_frames": chunk, "streams": ns, "calls": (n + chunk - 1) // chunk,
                               "ms_median": round(ts[len(ts) // 2], 4), "ms_min": round(ts[0], 4),
                               "items_equal": same}), flush=True)
     sys.exit(1 if bad else 0)
