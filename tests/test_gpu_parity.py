@@ -730,3 +730,37 @@ def test_release_stream_scratch(engine):
         b = [t.cpu() for t in engine.parse_varlen(d, o, valid, stream=s)]
     engine.release_stream(s)
     assert all(torch.equal(x, y) for x, y in zip(a, b))
+
+
+def test_empty_batches(engine):
+    """n = 0 on every batch entry point (a receive loop's empty recvmmsg batch): UFC_OK, nothing read or
+    written, no launch -- with NULL buffers, as an empty Vec's pointer may be."""
+    import ctypes
+    from uflow_amd import _native as NN
+    lib, ctx, z = NN.lib(), engine._ctx, None
+    s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    calls = {
+        "crc_fixed": lambda: lib.ufc_crc_batch_fixed(ctx, z, 1500, 1500, 0, z, z, s),
+        "crc_varlen": lambda: lib.ufc_crc_batch_varlen(ctx, z, z, 0, z, z, s),
+        "crc_pairs": lambda: lib.ufc_crc_batch_pairs(ctx, z, 0, z, 0, z, z, s),
+        "seal_fixed": lambda: lib.ufc_seal_batch_fixed(ctx, z, 1500, 1500, 0, z, s),
+        "seal_varlen": lambda: lib.ufc_seal_batch_varlen(ctx, z, z, 0, z, s),
+        "parse_varlen": lambda: lib.ufc_parse_batch_varlen(ctx, z, z, 0, z, z, z, 0, z, s),
+        "validate_host_varlen": lambda: lib.ufc_validate_host_varlen(ctx, z, z, 0, z, z),
+        "validate_host_slots": lambda: lib.ufc_validate_host_slots(ctx, z, 1472, z, 0, z, z),
+        "seal_host_slots": lambda: lib.ufc_seal_host_slots(ctx, z, 1472, z, 0, z),
+        "seal_host_varlen": lambda: lib.ufc_seal_host_varlen(ctx, z, z, 0, z),
+    }
+    rcs = {k: f() for k, f in calls.items()}
+    assert all(rc == 0 for rc in rcs.values()), rcs
+    torch.cuda.synchronize()
+    # and through the Python layer: empty tensors in, empty results out
+    d = torch.zeros(0, dtype=torch.uint8, device=DEV)
+    o = torch.zeros(1, dtype=torch.int64, device=DEV)
+    crc, valid = engine.crc_varlen(d, o)
+    assert crc.numel() == 0 and valid.numel() == 0
+    crc, valid = engine.crc_fixed(d, 1500, n=0)
+    assert crc.numel() == 0 and valid.numel() == 0
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    assert infos.shape[0] == 0 and int(used.cpu()[0]) == 0

@@ -983,9 +983,9 @@ void put_trailer(uint8_t* f, size_t len, uint32_t crc) {  // serial/mod.rs:466-4
 
 int ufc_seal_host_slots(ufc_ctx* ctx, uint8_t* h_slots, size_t slot_stride, const uint32_t* h_lens, size_t n,
                         uint32_t* h_crc_scratch) {
-  if (!ctx || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
-  if (n == 0) return UFC_OK;
-  if (!h_slots || !h_lens) return UFC_ERR_INVALID_ARG;
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;  // (an empty batch: nothing to do, whatever the pointers)
+  if (!h_slots || !h_lens || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
   for (size_t i = 0; i < n; i++)
     if (h_lens[i] < 4) return UFC_ERR_INVALID_ARG;
   // The gate computes crc = compute(frame[..len-4]) whatever the trailer holds: that is the seal.
@@ -997,9 +997,9 @@ int ufc_seal_host_slots(ufc_ctx* ctx, uint8_t* h_slots, size_t slot_stride, cons
 
 int ufc_seal_host_varlen(ufc_ctx* ctx, uint8_t* h_bytes, const uint64_t* h_offsets, size_t n,
                          uint32_t* h_crc_scratch) {
-  if (!ctx || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
-  if (n == 0) return UFC_OK;
-  if (!h_bytes || !h_offsets) return UFC_ERR_INVALID_ARG;
+  if (!ctx) return UFC_ERR_INVALID_ARG;
+  if (n == 0) return UFC_OK;  // (an empty batch: nothing to do, whatever the pointers)
+  if (!h_bytes || !h_offsets || !h_crc_scratch) return UFC_ERR_INVALID_ARG;
   for (size_t i = 0; i < n; i++)
     if (h_offsets[i + 1] < h_offsets[i] + 4) return UFC_ERR_INVALID_ARG;
   const int rc = ufc_validate_host_varlen(ctx, h_bytes, h_offsets, n, h_crc_scratch, nullptr);
