@@ -30,6 +30,8 @@
  *         crc_out[i]   = compute(frame_i[0 .. len_i-4])      (compute(frame_i) when len_i < 4)
  *         valid_out[i] = len_i >= 5 && crc_out[i] == BE32(frame_i[len_i-4 .. len_i])
  *     and the seal writes BE32(compute(frame_i[0 .. len_i-4])) into frame_i[len_i-4 .. len_i].
+ *   - An empty batch (n = 0) is nothing to do: every batch entry point returns UFC_OK for it with
+ *     a valid context, whatever its buffer pointers (an empty Vec's may be dangling or NULL).
  *   - Device entry points are asynchronous on `stream` (a hipStream_t, or NULL for the null
  *     stream), allocate nothing per call, and never fall back to the CPU: without a usable
  *     MI355X (gfx950) device ufc_ctx_create fails with UFC_ERR_NO_DEVICE.
