@@ -29,6 +29,16 @@ class FrameCrcEngine:
         self._ctx = ctypes.c_void_p()
         check(lib().ufc_ctx_create(ctypes.byref(self._ctx), self.device.index or 0), "ufc_ctx_create")
 
+    def _bytes_ptr(self, t):
+        """The frame bytes' pointer for the C ABI, which wants a readable device buffer even when a
+        batch holds only empty frames (torch gives an empty tensor a NULL data_ptr): a zeroed 256-B
+        buffer of the engine's stands in then."""
+        if t.numel():
+            return _ptr(t)
+        if getattr(self, "_no_bytes", None) is None:
+            self._no_bytes = torch.zeros(256, dtype=torch.uint8, device=self.device)
+        return _ptr(self._no_bytes)
+
     def close(self):
         if self._ctx:
             lib().ufc_ctx_destroy(self._ctx)
@@ -91,7 +101,7 @@ class FrameCrcEngine:
             valid_out = torch.empty(n, dtype=torch.uint8, device=self.device)
         self._check("frames", frames, (torch.uint8,), (n - 1) * stride + frame_len if n else 0)
         self._check_outputs(n, crc_out, valid_out)
-        check(lib().ufc_crc_batch_fixed(self._ctx, _ptr(frames), stride, frame_len, n, _ptr(crc_out),
+        check(lib().ufc_crc_batch_fixed(self._ctx, self._bytes_ptr(frames), stride, frame_len, n, _ptr(crc_out),
                                         _ptr(valid_out), self._stream(stream)), "ufc_crc_batch_fixed")
         return crc_out, valid_out
 
@@ -101,7 +111,7 @@ class FrameCrcEngine:
             n = (frames.numel() - frame_len) // stride + 1 if frames.numel() >= frame_len else 0
         self._check("frames", frames, (torch.uint8,), (n - 1) * stride + frame_len if n else 0)
         self._check_outputs(n, crc_out)
-        check(lib().ufc_seal_batch_fixed(self._ctx, _ptr(frames), stride, frame_len, n, _ptr(crc_out),
+        check(lib().ufc_seal_batch_fixed(self._ctx, self._bytes_ptr(frames), stride, frame_len, n, _ptr(crc_out),
                                          self._stream(stream)), "ufc_seal_batch_fixed")
         return crc_out
 
@@ -117,7 +127,7 @@ class FrameCrcEngine:
         self._check("offsets", offsets, (torch.int64,), 1)
         self._check("data", data, (torch.uint8,), 0)
         self._check_outputs(n, crc_out, valid_out)
-        check(lib().ufc_crc_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(crc_out), _ptr(valid_out),
+        check(lib().ufc_crc_batch_varlen(self._ctx, self._bytes_ptr(data), _ptr(offsets), n, _ptr(crc_out), _ptr(valid_out),
                                          self._stream(stream)), "ufc_crc_batch_varlen")
         return crc_out, valid_out
 
@@ -126,7 +136,7 @@ class FrameCrcEngine:
         self._check("offsets", offsets, (torch.int64,), 1)
         self._check("data", data, (torch.uint8,), 0)
         self._check_outputs(n, crc_out)
-        check(lib().ufc_seal_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(crc_out),
+        check(lib().ufc_seal_batch_varlen(self._ctx, self._bytes_ptr(data), _ptr(offsets), n, _ptr(crc_out),
                                           self._stream(stream)), "ufc_seal_batch_varlen")
         return crc_out
 
@@ -142,7 +152,7 @@ class FrameCrcEngine:
         self._check("pairs", pairs, (torch.int64,), 2 * n)
         self._check("data", data, (torch.uint8,), 0)
         self._check_outputs(n, crc_out, valid_out)
-        check(lib().ufc_crc_batch_pairs(self._ctx, _ptr(data), data.numel(), _ptr(pairs), n, _ptr(crc_out),
+        check(lib().ufc_crc_batch_pairs(self._ctx, self._bytes_ptr(data), data.numel(), _ptr(pairs), n, _ptr(crc_out),
                                         _ptr(valid_out), self._stream(stream)), "ufc_crc_batch_pairs")
         return crc_out, valid_out
 
@@ -172,7 +182,7 @@ class FrameCrcEngine:
         infos = torch.empty((max(n, 0), 32), dtype=torch.uint8, device=self.device)
         items = torch.empty((items_cap, 24), dtype=torch.uint8, device=self.device)
         used = torch.zeros(1, dtype=torch.int64, device=self.device)
-        check(lib().ufc_parse_batch_varlen(self._ctx, _ptr(data), _ptr(offsets), n, _ptr(valid), _ptr(infos),
+        check(lib().ufc_parse_batch_varlen(self._ctx, self._bytes_ptr(data), _ptr(offsets), n, _ptr(valid), _ptr(infos),
                                            _ptr(items), items_cap, _ptr(used), self._stream(stream)),
               "ufc_parse_batch_varlen")
         return infos, items, used
