@@ -82,3 +82,52 @@ def test_fixed_gate_and_seal(engine, frame_len, extra, n, seed):
     torch.cuda.synchronize()
     assert np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc)
     assert np.array_equal(valid.cpu().numpy(), ref_valid)
+
+
+KINDS = st.sampled_from(["data", "recv", "ack", "sync", "ref"])
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(st.tuples(KINDS, st.integers(min_value=0, max_value=2**31), st.integers(min_value=0, max_value=3)),
+                min_size=1, max_size=400))
+def test_parse_vs_codec_oracle(engine, spec):
+    """Device gate + parse of a batch hypothesis composes from the codec oracle's frame generators
+    (kind, seed, damage: 0 none, 1 a flipped bit, 2 a damaged header byte resealed, 3 a truncated
+    frame resealed), every frame's info and items vs Frame::read of the oracle."""
+    import random
+    from oracle import codec as C
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE
+    from test_codec_cpu import info_to_dict
+    refs = C.reference_test_frames()
+    frames = []
+    for kind, seed, damage in spec:
+        rng = random.Random(seed)
+        f = {"data": lambda: C.random_data_frame(rng), "recv": lambda: C.receive_side_data_frame(rng),
+             "ack": lambda: C.random_ack_frame(rng, 40), "sync": lambda: C.random_sync_frame(rng),
+             "ref": lambda: refs[seed % len(refs)][1]}[kind]()
+        fb = bytearray(C.frame_write(f))
+        if damage == 1:
+            fb[rng.randrange(len(fb))] ^= 1 << rng.randrange(8)
+        elif damage == 2 and len(fb) > 6:
+            fb[rng.randrange(1, min(len(fb) - 4, 40))] = rng.getrandbits(8)
+            fb[-4:] = oracle.compute(bytes(fb[:-4])).to_bytes(4, "big")
+        elif damage == 3 and len(fb) > 9:
+            fb = fb[:rng.randrange(5, len(fb) - 4)] + b"\0\0\0\0"
+            fb[-4:] = oracle.compute(bytes(fb[:-4])).to_bytes(4, "big")
+        frames.append(bytes(fb))
+    offsets = np.zeros(len(frames) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum([len(f) for f in frames])
+    d = torch.from_numpy(np.frombuffer(b"".join(frames), dtype=np.uint8).copy()).to(DEV)
+    o = torch.from_numpy(offsets).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    infos = infos.cpu().numpy().view(FRAME_INFO_DTYPE).reshape(-1)
+    items = items.cpu().numpy().view(ITEM_DTYPE).reshape(-1)
+    total = 0
+    for i, fb in enumerate(frames):
+        cnt = int(infos[i]["item_count"]) if infos[i]["ok"] else 0
+        assert int(infos[i]["item_first"]) == total
+        assert info_to_dict(infos[i], items[total:total + cnt], fb) == C.frame_read(fb), i
+        total += cnt
+    assert int(used.cpu()[0]) == total
