@@ -278,7 +278,10 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   }
 }
 
-template <int U, int X4>
+// The emit's header loads leave nothing behind for later (each line is read once, by neighbouring lanes
+// of one instruction): non-temporal (buffer-load aux 2; the walk's loads stay default, measured slower).
+constexpr int kEmitAux = 2;
+template <int U, int X4, int AUX = 0>
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
     const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
@@ -368,7 +371,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
           const uint32_t al = ex & ~3u;
           if (X4 == 2 && ex + 16 <= (uint32_t)range) {  // one unaligned 16-byte load at the header
             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)ex, 0, 0);
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)ex, 0, AUX);
             x[u][0] = v.x, x[u][1] = v.y, x[u][2] = v.z, x[u][3] = v.w;
             x[u][4] = 0;
           } else if constexpr (X4 >= 1) {
@@ -489,10 +492,10 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
   if (e != hipSuccess) return e;
-  // One item per thread per round, one 16-byte load per header (0.526 against 0.551 ms with five
-  // dword loads; 4 items per round 0.532 with them, 0.543 without; the exact-offset load 0.453
-  // against 0.458 for the aligned pair: DESIGN.md section 5.5).
-  auto emit = parse_emit_kernel<1, 2>;
+  // One item per thread per round, one non-temporal 16-byte load per header (0.526 against 0.551 ms
+  // with five dword loads; 4 items per round 0.532 with them, 0.543 without; the exact-offset load
+  // 0.453 against 0.458 for the aligned pair; non-temporal 0.447 against 0.453: DESIGN.md section 5.5).
+  auto emit = parse_emit_kernel<1, 2, kEmitAux>;
 #ifdef UFC_TUNING
   {  // UFC_EMIT_U=1|2|4 items per thread per round, UFC_EMIT_X4=0: five dword loads per header,
      // 2: one unaligned 16-byte load at the header
@@ -502,7 +505,9 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
     const int x4 = wx ? std::atoi(wx) : 2;
     if (eu == 2) emit = x4 == 2 ? parse_emit_kernel<2, 2> : x4 ? parse_emit_kernel<2, 1> : parse_emit_kernel<2, 0>;
     else if (eu == 4) emit = x4 == 2 ? parse_emit_kernel<4, 2> : x4 ? parse_emit_kernel<4, 1> : parse_emit_kernel<4, 0>;
-    else emit = x4 == 2 ? parse_emit_kernel<1, 2> : x4 ? parse_emit_kernel<1, 1> : parse_emit_kernel<1, 0>;
+    else emit = x4 == 2 ? parse_emit_kernel<1, 2, kEmitAux> : x4 ? parse_emit_kernel<1, 1> : parse_emit_kernel<1, 0>;
+    if (const char* w = std::getenv("UFC_EMIT_AUX"))  // cache policy of the header loads (0: default)
+      emit = std::atoi(w) == 0 ? parse_emit_kernel<1, 2, 0> : parse_emit_kernel<1, 2, kEmitAux>;
   }
 #endif
   emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
