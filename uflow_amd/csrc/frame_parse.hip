@@ -95,14 +95,24 @@ static_assert(sizeof(ufc_item) == 24 && offsetof(ufc_item, channel_id) == 4 && o
                   offsetof(ufc_item, flags) == 14 && offsetof(ufc_item, data_offset) == 16 &&
                   offsetof(ufc_item, data_len) == 20,
               "ufc_item layout");
+template <bool NT = false>  // NT: non-temporal stores
 __device__ __forceinline__ void store_item(ufc_item* p, const ufc_item& it) {
   typedef __attribute__((address_space(1))) uint64_t g_u64w;
   g_u64w* q = (g_u64w*)p;
-  q[0] = (uint64_t)it.id | ((uint64_t)it.channel_id << 32) | ((uint64_t)it.form << 40) |
-         ((uint64_t)it.window_parent_lead << 48);
-  q[1] = (uint64_t)it.channel_parent_lead | ((uint64_t)it.fragment_id << 16) | ((uint64_t)it.fragment_id_last << 32) |
-         ((uint64_t)it.flags << 48);
-  q[2] = (uint64_t)it.data_offset | ((uint64_t)it.data_len << 32);
+  const uint64_t w0 = (uint64_t)it.id | ((uint64_t)it.channel_id << 32) | ((uint64_t)it.form << 40) |
+                      ((uint64_t)it.window_parent_lead << 48);
+  const uint64_t w1 = (uint64_t)it.channel_parent_lead | ((uint64_t)it.fragment_id << 16) |
+                      ((uint64_t)it.fragment_id_last << 32) | ((uint64_t)it.flags << 48);
+  const uint64_t w2 = (uint64_t)it.data_offset | ((uint64_t)it.data_len << 32);
+  if constexpr (NT) {
+    __builtin_nontemporal_store(w0, q);
+    __builtin_nontemporal_store(w1, q + 1);
+    __builtin_nontemporal_store(w2, q + 2);
+  } else {
+    q[0] = w0;
+    q[1] = w1;
+    q[2] = w2;
+  }
 }
 struct PackedSink {
   static constexpr bool kDecode = true;
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
 // The emit's header loads leave nothing behind for later (each line is read once, by neighbouring lanes
 // of one instruction): non-temporal (buffer-load aux 2; the walk's loads stay default, measured slower).
 constexpr int kEmitAux = 2;
-template <int U, int X4, int AUX = 0>
+template <int U, int X4, int AUX = 0, bool NTS = false>
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
     const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
@@ -414,7 +424,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
         } else {
           ufc_codec::decode_ack_group(h, it);
         }
-        store_item(items + gb + (uint64_t)u * kParseThreads, it);
+        store_item<NTS>(items + gb + (uint64_t)u * kParseThreads, it);
       }
     }
     // Frames whose headers did not fit the slots: walked again, items stored directly.
@@ -492,10 +502,11 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   if (e != hipSuccess) return e;
   e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
   if (e != hipSuccess) return e;
-  // One item per thread per round, one non-temporal 16-byte load per header (0.526 against 0.551 ms
-  // with five dword loads; 4 items per round 0.532 with them, 0.543 without; the exact-offset load
-  // 0.453 against 0.458 for the aligned pair; non-temporal 0.447 against 0.453: DESIGN.md section 5.5).
-  auto emit = parse_emit_kernel<1, 2, kEmitAux>;
+  // One item per thread per round, one non-temporal 16-byte load per header, non-temporal record
+  // stores (0.526 against 0.551 ms with five dword loads; 4 items per round 0.532 with them, 0.543
+  // without; the exact-offset load 0.453 against 0.458 for the aligned pair; non-temporal loads 0.447
+  // against 0.453; non-temporal stores 0.426 against 0.430 on a faster box: DESIGN.md section 5.5).
+  auto emit = parse_emit_kernel<1, 2, kEmitAux, true>;
 #ifdef UFC_TUNING
   {  // UFC_EMIT_U=1|2|4 items per thread per round, UFC_EMIT_X4=0: five dword loads per header,
      // 2: one unaligned 16-byte load at the header
@@ -505,9 +516,11 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
     const int x4 = wx ? std::atoi(wx) : 2;
     if (eu == 2) emit = x4 == 2 ? parse_emit_kernel<2, 2> : x4 ? parse_emit_kernel<2, 1> : parse_emit_kernel<2, 0>;
     else if (eu == 4) emit = x4 == 2 ? parse_emit_kernel<4, 2> : x4 ? parse_emit_kernel<4, 1> : parse_emit_kernel<4, 0>;
-    else emit = x4 == 2 ? parse_emit_kernel<1, 2, kEmitAux> : x4 ? parse_emit_kernel<1, 1> : parse_emit_kernel<1, 0>;
+    else emit = x4 == 2 ? parse_emit_kernel<1, 2, kEmitAux, true> : x4 ? parse_emit_kernel<1, 1> : parse_emit_kernel<1, 0>;
     if (const char* w = std::getenv("UFC_EMIT_AUX"))  // cache policy of the header loads (0: default)
-      emit = std::atoi(w) == 0 ? parse_emit_kernel<1, 2, 0> : parse_emit_kernel<1, 2, kEmitAux>;
+      emit = std::atoi(w) == 0 ? parse_emit_kernel<1, 2, 0, true> : parse_emit_kernel<1, 2, kEmitAux, true>;
+    if (const char* w = std::getenv("UFC_EMIT_NTSTORE"))  // 0: the item records' stores default policy
+      if (std::atoi(w) == 0) emit = parse_emit_kernel<1, 2, kEmitAux, false>;
   }
 #endif
   emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
