@@ -8,7 +8,8 @@
 //             LDS while the thread walks (no global store inside the dependent load chain), then
 //             written compactly per workgroup.  Only the bytes the walk needs are read (each
 //             datagram's first byte and its length bytes).
-//   2. scan:  exclusive sum of the item counts (hipcub) -> each frame's first item.
+//   2. scan:  exclusive sum of the workgroups' item counts (hipcub) -> each workgroup's first item
+//             (the emit adds the counts of the frames before a frame within its workgroup).
 //   3. emit:  item-parallel over the workgroup's item range: lane j finds its frame (binary search
 //             over the firsts in LDS), loads the header bytes (independent 4-byte loads across
 //             items), decodes the ufc_item (datagram with datagram_is_valid of
@@ -42,6 +43,8 @@ constexpr uint64_t kSegWords = (uint64_t)kPosSlots * kParseThreads;  // u16 per 
 enum : uint8_t { kItemsNone = 0, kItemsPos = 1, kItemsAck = 2, kItemsWalk = 3 };
 
 typedef hipcub::BlockScan<uint32_t, kParseThreads> BlockScan;
+// Two per-frame counts scanned at once (each workgroup sum < 2^32: 256 frames x < 2^24), low and high halves.
+typedef hipcub::BlockScan<uint64_t, kParseThreads> BlockScan2;
 
 // Byte-aligned global views: the IR carries align 1, so the compiler never assumes 4- or 8-byte
 // alignment when it combines or splits these loads; gfx950's unaligned access mode still makes each
@@ -134,14 +137,15 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
                                                                    ufc_frame_info* infos, uint32_t* counts,
                                                                    uint8_t* modes, uint16_t* pos_seg,
                                                                    unsigned long long* seg_cursor, uint32_t* seg_base,
-                                                                   uint64_t seg_cap) {
+                                                                   uint64_t seg_cap, uint32_t* wg_counts) {
   __shared__ uint16_t slots[kSegWords];
-  __shared__ typename BlockScan::TempStorage scan_tmp;
+  __shared__ typename BlockScan2::TempStorage scan_tmp;
   __shared__ uint32_t base_lds;
   const uint32_t t = threadIdx.x;
   const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + t;
   uint32_t npos = 0;
   uint8_t mode = kItemsNone;
+  uint32_t cnt_all = 0;
   if (i < n) {
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
@@ -162,9 +166,13 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t
     info.item_first = 0;  // written by the emit step
     infos[i] = info;
     counts[i] = cnt;
+    cnt_all = cnt;
   }
-  uint32_t lo, total;
-  BlockScan(scan_tmp).ExclusiveSum(npos, lo, total);
+  // header slots (low half) and items (high half) of the workgroup's frames, one scan
+  uint64_t lo2, total2;
+  BlockScan2(scan_tmp).ExclusiveSum((uint64_t)npos | ((uint64_t)cnt_all << 32), lo2, total2);
+  const uint32_t lo = (uint32_t)lo2, total = (uint32_t)total2;
+  if (t == 0) wg_counts[blockIdx.x] = (uint32_t)(total2 >> 32);  // (scanned over the workgroups next)
   // the workgroup's segment of header slots, from the launch's bump counter (no room: the emit
   // step re-walks this workgroup's frames instead)
   if (t == 0) {
@@ -228,10 +236,10 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
                                                                         ufc_frame_info* infos, uint32_t* counts,
                                                                         uint8_t* modes, uint16_t* pos_seg,
                                                                         unsigned long long* seg_cursor, uint32_t* seg_base,
-                                                                        uint64_t seg_cap) {
+                                                                        uint64_t seg_cap, uint32_t* wg_counts) {
   __shared__ uint16_t slots[kInlineSlots * kParseThreads];
   __shared__ uint32_t pool[kPoolSlots];
-  __shared__ typename BlockScan::TempStorage scan_tmp;
+  __shared__ typename BlockScan2::TempStorage scan_tmp;
   __shared__ uint32_t base_lds, pool_ctr;
   const uint32_t t = threadIdx.x;
   const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + t;
@@ -240,6 +248,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
   uint32_t npos = 0, head = kPoolNil, tail = kPoolNil;
   bool full = false;
   uint8_t mode = kItemsNone;
+  uint32_t cnt_all = 0;
   if (i < n) {
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
@@ -262,9 +271,13 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     info.item_first = 0;  // written by the emit step
     infos[i] = info;
     counts[i] = cnt;
+    cnt_all = cnt;
   }
-  uint32_t lo, total;
-  BlockScan(scan_tmp).ExclusiveSum(npos, lo, total);
+  // header slots (low half) and items (high half) of the workgroup's frames, one scan
+  uint64_t lo2, total2;
+  BlockScan2(scan_tmp).ExclusiveSum((uint64_t)npos | ((uint64_t)cnt_all << 32), lo2, total2);
+  const uint32_t lo = (uint32_t)lo2, total = (uint32_t)total2;
+  if (t == 0) wg_counts[blockIdx.x] = (uint32_t)(total2 >> 32);  // (scanned over the workgroups next)
   if (t == 0) {
     // (64-bit cursor: the sum of every workgroup's total may pass 2^32 long after the cap is reached)
     const unsigned long long b64 = total ? atomicAdd(seg_cursor, (unsigned long long)total) : 0ull;
@@ -294,29 +307,34 @@ constexpr int kEmitAux = 2;
 template <int U, int X4, int AUX = 0, bool NTS = false>
 __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
     const uint8_t* bytes, const uint64_t* offsets, uint64_t n, const uint8_t* valid, ufc_frame_info* infos,
-    const uint32_t* counts, const uint32_t* firsts, const uint8_t* modes, const uint16_t* pos_seg,
+    const uint32_t* counts, const uint32_t* wg_firsts, const uint8_t* modes, const uint16_t* pos_seg,
     const uint32_t* seg_base, ufc_item* items, uint64_t cap, uint64_t* items_used) {
   __shared__ uint32_t lfirst[kParseThreads], lseg[kParseThreads];
   __shared__ uint64_t lstart[kParseThreads];
   __shared__ uint8_t lmode[kParseThreads];
   __shared__ uint32_t lend;
-  __shared__ typename BlockScan::TempStorage scan_tmp;
+  __shared__ typename BlockScan2::TempStorage scan_tmp;
   const uint32_t t = threadIdx.x;
   const uint64_t i0 = (uint64_t)blockIdx.x * kParseThreads, i = i0 + t;
   const uint32_t nb = (uint32_t)min((uint64_t)kParseThreads, n - i0);  // frames of this workgroup
-  uint32_t first = 0, cnt = 0;
+  uint32_t cnt = 0;
   uint8_t mode = kItemsNone;
   uint64_t a = 0;
   if (i < n) {
-    first = firsts[i];
     cnt = counts[i];
     mode = modes[i];
     a = offsets[i];
+  }
+  // each frame's first item (the workgroup's first from the scan over workgroups + the items of the
+  // frames before it here) and its header slots' offset in the workgroup's segment, one scan
+  uint64_t lo2;
+  BlockScan2(scan_tmp).ExclusiveSum((uint64_t)(mode == kItemsPos ? cnt : 0u) | ((uint64_t)cnt << 32), lo2);
+  const uint32_t lo = (uint32_t)lo2;
+  const uint32_t first = wg_firsts[blockIdx.x] + (uint32_t)(lo2 >> 32);
+  if (i < n) {
     infos[i].item_first = first;
     if (i == n - 1 && items_used) *items_used = (uint64_t)first + cnt;
   }
-  uint32_t lo;
-  BlockScan(scan_tmp).ExclusiveSum(mode == kItemsPos ? cnt : 0u, lo);
   lfirst[t] = first;
   lseg[t] = lo;
   lstart[t] = a;
@@ -442,7 +460,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
 
 namespace {
 struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned parts)
-  uint64_t counts, firsts, modes, cursor, bases, slots, temp, end, seg_cap;
+  uint64_t counts, wg_counts, wg_firsts, modes, cursor, bases, slots, temp, end, seg_cap;
   ParseLayout(uint64_t n, uint64_t items_cap, size_t temp_bytes) {
     auto up = [](uint64_t b) { return (b + 255) / 256 * 256; };
     const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
@@ -451,8 +469,9 @@ struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned pa
     seg_cap = std::min<uint64_t>(std::min<uint64_t>(n * kPosSlots, std::max<uint64_t>(items_cap, 1)),
                                  0xFFFFFFFEull - kSegWords);
     counts = 0;
-    firsts = counts + up(n * 4);
-    modes = firsts + up(n * 4);
+    wg_counts = counts + up(n * 4);  // items per workgroup of 256 frames, then their exclusive sum
+    wg_firsts = wg_counts + up(blocks * 4);
+    modes = wg_firsts + up(blocks * 4);
     cursor = modes + up(n);
     bases = cursor + 256;
     slots = bases + up(blocks * 4);
@@ -460,9 +479,10 @@ struct ParseLayout {  // the scratch of a parse of n frames (256-byte aligned pa
     end = temp + up(temp_bytes);
   }
 };
-size_t scan_temp_bytes(uint64_t n) {
+size_t scan_temp_bytes(uint64_t n) {  // the scan over the workgroups' item counts
+  const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
   size_t temp = 0;
-  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)blocks);
   return temp;
 }
 }  // namespace
@@ -478,7 +498,8 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   if (lay.end > scratch_bytes) return hipErrorInvalidValue;
   char* s = (char*)scratch;
   uint32_t* counts = (uint32_t*)(s + lay.counts);
-  uint32_t* firsts = (uint32_t*)(s + lay.firsts);
+  uint32_t* wg_counts = (uint32_t*)(s + lay.wg_counts);
+  uint32_t* wg_firsts = (uint32_t*)(s + lay.wg_firsts);
   uint8_t* modes = (uint8_t*)(s + lay.modes);
   unsigned long long* cursor = (unsigned long long*)(s + lay.cursor);
   uint32_t* bases = (uint32_t*)(s + lay.bases);
@@ -494,13 +515,15 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   if (pool)
     parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
                                                                            counts, modes, pos_seg, cursor, bases,
-                                                                           lay.seg_cap);
+                                                                           lay.seg_cap, wg_counts);
   else
     parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
-                                                                      modes, pos_seg, cursor, bases, lay.seg_cap);
+                                                                      modes, pos_seg, cursor, bases, lay.seg_cap,
+                                                                      wg_counts);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, firsts, (int)n, stream);
+  // each workgroup's first item (the emit adds the frames' own counts within the workgroup)
+  e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, wg_counts, wg_firsts, (int)blocks, stream);
   if (e != hipSuccess) return e;
   // One item per thread per round, one non-temporal 16-byte load per header, non-temporal record
   // stores (0.526 against 0.551 ms with five dword loads; 4 items per round 0.532 with them, 0.543
@@ -524,7 +547,7 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   }
 #endif
   emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
-                                                                    firsts, modes, pos_seg, bases, a.items, a.items_cap,
+                                                                    wg_firsts, modes, pos_seg, bases, a.items, a.items_cap,
                                                                     a.items_used);
   return hipGetLastError();
 }
