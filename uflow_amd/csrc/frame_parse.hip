@@ -64,20 +64,39 @@ struct DevBytes {
   }
 };
 
-// The walk's reader: the frame's first 8 bytes (kind, the data header's fields) come from one 8-byte
-// load issued with the frame's other first reads when the frame has 8 bytes; the rest as DevBytes.
+// The walk's reader: the frame's first 14 bytes (kind, the data header's fields and the first
+// datagram's size bytes; every field of an ack frame's header) come from two 8-byte loads issued
+// together (bytes 0..7 and 6..13) when the frame has 14 bytes, bytes 0..7 from one when it has 8 to
+// 13; the rest as DevBytes.  held_byte keeps every shift amount in range: an out-of-range shift in
+// the unselected arm of a ternary let the compiler treat a byte as undefined (data frames failing
+// at random, profiles/EXPERIMENTS.md).
 struct DevBytesHead {
   const uint8_t* p;
-  uint64_t w;  // bytes 0..7, little-endian
-  bool has8;
-  __device__ static uint64_t load8(const uint8_t* q) {  // (any byte address: unaligned access mode)
-    return *(g_u64_a1*)q;
+  uint64_t w0, w1;  // bytes 0..7 and 6..13, little-endian
+  uint32_t held;    // bytes 0 .. held-1 in w0/w1: 14, 8 or 0
+  __device__ static DevBytesHead load(const uint8_t* q, uint32_t len) {  // (any byte address: unaligned access mode)
+    DevBytesHead r{q, 0ull, 0ull, 0u};
+    if (len >= 8) {
+      r.w0 = *(g_u64_a1*)q;
+      r.held = 8;
+    }
+    if (len >= 14) {
+      r.w1 = *(g_u64_a1*)(q + 6);
+      r.held = 14;
+    }
+    return r;
+  }
+  __device__ uint32_t held_byte(uint32_t i) const {  // (shift amounts always in range)
+    const uint64_t w = i < 8 ? w0 : w1;
+    const uint32_t b = (i < 8 ? i : i - 6) & 7u;
+    return (uint32_t)(w >> (8 * b)) & 0xFFu;
   }
   __device__ uint32_t operator()(uint32_t i) const {
-    if (has8 && i < 8) return (uint32_t)(w >> (8 * i)) & 0xFFu;
+    if (i < held) return held_byte(i);
     return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
   }
   __device__ uint32_t head3(uint32_t i) const {
+    if (i + 3 <= held) return held_byte(i) | (held_byte(i + 1) << 8) | (held_byte(i + 2) << 16);
     return *(g_u32_a1*)(p + i) & 0xFFFFFFu;
   }
 };
@@ -253,8 +272,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
-    const bool has8 = len >= 8;
-    const DevBytesHead rd{bytes + a, has8 ? DevBytesHead::load8(bytes + a) : 0ull, has8};
+    const DevBytesHead rd = DevBytesHead::load(bytes + a, len);
     const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
     const uint32_t cnt = ok ? info.item_count : 0u;
