@@ -132,12 +132,17 @@ __device__ __forceinline__ uint4 front_fix(uint4 x, int p, uint32_t G) {
   const uint32_t pc = (uint32_t)min(max(p, 0), 20);
   const uint32_t s = 8u * pc;  // data bytes start at bit s of the 128-bit lane
   const uint64_t lo = (uint64_t)x.x | ((uint64_t)x.y << 32), hi = (uint64_t)x.z | ((uint64_t)x.w << 32);
-  const uint64_t mlo = s >= 64u ? 0ull : ~0ull << s;
-  const uint64_t mhi = s >= 128u ? 0ull : (s <= 64u ? ~0ull : ~0ull << (s - 64u));
+  // (every shift amount masked into range, also in the arms a ternary does not select: an out-of-range
+  // amount there is poison the compiler may propagate)
+  const uint64_t mlo = s >= 64u ? 0ull : ~0ull << (s & 63u);
+  const uint64_t mhi = s >= 128u ? 0ull : (s <= 64u ? ~0ull : ~0ull << ((s - 64u) & 63u));
   const int q = (int)pc - 4;  // G's first byte in the lane: -4..16
   const uint64_t g = G;
-  const uint64_t glo = q < 0 ? (g >> ((uint32_t)(-8 * q) & 63u)) & (q == -4 ? 0ull : ~0ull) : (q < 8 ? g << (8 * q) : 0ull);
-  const uint64_t ghi = q <= 4 ? 0ull : (q < 8 ? g >> (64 - 8 * q) : (q < 16 ? g << (8 * (q - 8)) : 0ull));
+  const uint64_t glo = q < 0 ? (g >> ((uint32_t)(-8 * q) & 63u)) & (q == -4 ? 0ull : ~0ull)
+                             : (q < 8 ? g << ((uint32_t)(8 * q) & 63u) : 0ull);
+  const uint64_t ghi = q <= 4 ? 0ull
+                              : (q < 8 ? g >> ((uint32_t)(64 - 8 * q) & 63u)
+                                       : (q < 16 ? g << ((uint32_t)(8 * (q - 8)) & 63u) : 0ull));
   const uint64_t rlo = (lo & mlo) | glo, rhi = (hi & mhi) | ghi;
   return make_uint4((uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32));
 }

@@ -68,7 +68,7 @@ __device__ __forceinline__ uint32_t vl_sel(uint32_t g) { return 0x03020100u + (4
 // Front fix of a word of block 0 (or word 0 of block 1): d = bytes of the word that precede the
 // frame.  Bytes at frame offsets [-4, 0) are G's, below -4 zeros: x' = (x & dm) | pre.
 __device__ __forceinline__ uint32_t vl_fix(uint32_t x, int d, uint32_t G) {
-  const uint32_t dm = d <= 0 ? 0xFFFFFFFFu : (d < 4 ? (0xFFFFFFFFu << (8 * d)) : 0u);
+  const uint32_t dm = d <= 0 ? 0xFFFFFFFFu : (d < 4 ? (0xFFFFFFFFu << ((uint32_t)(8 * d) & 31u)) : 0u);
   const uint32_t pre = (d > 0 && d < 8) ? (uint32_t)(((uint64_t)G << 32) >> ((64 - 8 * d) & 63)) : 0u;
   return __builtin_amdgcn_bitop3_b32(x, dm, pre, 0xEA);  // (x & dm) | pre
 }

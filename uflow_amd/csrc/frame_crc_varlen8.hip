@@ -542,7 +542,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       for (int i = 0; i < 4; i++) {
         const int ob = o + 4 * i;  // frame offset of the word's first byte
         const uint32_t lo = (uint32_t)min(max(-ob, 0), 4), hi = (uint32_t)min(max((int)d.len - ob, 0), 4);
-        const uint32_t mhi = hi >= 4u ? ~0u : ((1u << (8u * hi)) - 1u), mlo = lo >= 4u ? 0u : (~0u << (8u * lo));
+        const uint32_t mhi = hi >= 4u ? ~0u : ((1u << ((8u * hi) & 31u)) - 1u),  // (amounts kept in range)
+                       mlo = lo >= 4u ? 0u : (~0u << ((8u * lo) & 31u));
         x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh) & mhi & mlo;
       }
       return make_uint4(x[0], x[1], x[2], x[3]);
