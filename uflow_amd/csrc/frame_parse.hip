@@ -64,32 +64,33 @@ struct DevBytes {
   }
 };
 
-// The walk's reader: the frame's first 14 bytes (kind, the data header's fields and the first
-// datagram's size bytes; every field of an ack frame's header) come from two 8-byte loads issued
-// together (bytes 0..7 and 6..13) when the frame has 14 bytes, bytes 0..7 from one when it has 8 to
-// 13; the rest as DevBytes.  held_byte keeps every shift amount in range: an out-of-range shift in
-// the unselected arm of a ternary let the compiler treat a byte as undefined (data frames failing
-// at random, profiles/EXPERIMENTS.md).
+// The walk's reader: the frame's first 16 bytes (kind, the data header's fields and the first
+// datagram's size bytes; every field of an ack frame's header) come from one 16-byte load issued with
+// the frame's other first reads when the frame has 16 bytes, bytes 0..7 from one 8-byte load when it
+// has 8 to 15; the rest as DevBytes.  held_byte keeps every shift amount in range: an out-of-range
+// shift in the unselected arm of a ternary let the compiler treat a byte as undefined (data frames
+// failing at random, profiles/EXPERIMENTS.md).
+typedef unsigned int u32x4_h __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1), aligned(1))) u32x4_h g_u32x4_h;
 struct DevBytesHead {
   const uint8_t* p;
-  uint64_t w0, w1;  // bytes 0..7 and 6..13, little-endian
-  uint32_t held;    // bytes 0 .. held-1 in w0/w1: 14, 8 or 0
+  uint64_t w0, w1;  // bytes 0..7 and 8..15, little-endian
+  uint32_t held;    // bytes 0 .. held-1 in w0/w1: 16, 8 or 0
   __device__ static DevBytesHead load(const uint8_t* q, uint32_t len) {  // (any byte address: unaligned access mode)
     DevBytesHead r{q, 0ull, 0ull, 0u};
-    if (len >= 8) {
+    if (len >= 16) {
+      const u32x4_h v = *(g_u32x4_h*)q;
+      r.w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
+      r.w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
+      r.held = 16;
+    } else if (len >= 8) {
       r.w0 = *(g_u64_a1*)q;
       r.held = 8;
-    }
-    if (len >= 14) {
-      r.w1 = *(g_u64_a1*)(q + 6);
-      r.held = 14;
     }
     return r;
   }
   __device__ uint32_t held_byte(uint32_t i) const {  // (shift amounts always in range)
-    const uint64_t w = i < 8 ? w0 : w1;
-    const uint32_t b = (i < 8 ? i : i - 6) & 7u;
-    return (uint32_t)(w >> (8 * b)) & 0xFFu;
+    return (uint32_t)((i < 8 ? w0 : w1) >> (8 * (i & 7u))) & 0xFFu;
   }
   __device__ uint32_t operator()(uint32_t i) const {
     if (i < held) return held_byte(i);
