@@ -288,3 +288,27 @@ def test_varlen_claimed_runs_with_slow_sets(engine):
     crc, valid = engine.crc_pairs(d, torch.from_numpy(pairs).to(DEV))
     torch.cuda.synchronize()
     _compare(crc, valid, ref_crc[rev], ref_valid[rev], "claimed runs, pairs")
+
+
+def test_parse_large_batch(engine):
+    """A 4.32M-frame parse (the codec test batch tiled 7200 times, 16875 workgroups, 1.3 GB): every
+    frame's info and the item count against the native host parse."""
+    from test_gpu_parity import _codec_batch
+    from uflow_amd.frame import FRAME_INFO_DTYPE, parse_batch_host
+    _, data, offsets = _codec_batch(10, 600)
+    reps = 7200
+    lens = np.diff(offsets)
+    big = np.tile(data, reps)
+    offs = np.zeros(len(lens) * reps + 1, dtype=np.int64)
+    offs[1:] = np.cumsum(np.tile(lens, reps))
+    n = offs.size - 1
+    d = torch.from_numpy(big).to(DEV)
+    o = torch.from_numpy(offs).to(DEV)
+    _, valid = engine.crc_varlen(d, o)
+    infos, items, used = engine.parse_varlen(d, o, valid)
+    torch.cuda.synchronize()
+    got = _host(infos).view(FRAME_INFO_DTYPE).reshape(-1)
+    ref, ref_items = parse_batch_host(big, offs.astype(np.uint64), _host(valid), nthreads=THREADS)
+    bad = np.nonzero((got.view(np.uint8).reshape(n, -1) != ref.view(np.uint8).reshape(n, -1)).any(1))[0]
+    assert bad.size == 0, f"{bad.size} frame infos differ, first frames {bad[:8]}"
+    assert int(used.cpu()[0]) == ref_items.size
