@@ -65,6 +65,8 @@ def parse():
     ap.add_argument("--no-ceiling", action="store_true", help="skip the read-only streaming ceiling probe")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of each CPU baseline leg")
+    ap.add_argument("--no-n1-ref", action="store_true",
+                    help="N > 1: skip n1_sharded_ref (rank 0 alone gating the whole batch on its GPU)")
     return ap.parse_args()
 
 
@@ -292,6 +294,37 @@ def fake_worker(world, rank):
     dist.destroy_process_group()
 
 
+def n1_sharded_reference(eng, total, L, seed, flip_every, dev, steps=5):
+    """Config 4 at N = 1 on rank 0's GPU: the whole `total`-frame batch (or, when it does not fit beside
+    this rank's shard, the largest multiple of 1M frames that does, said so) gated in one call of
+    ufc_crc_batch_fixed -- what the N = 1 sharded path runs, since one rank has nothing to transfer --
+    timed with HIP events over `steps` calls; valid flags checked against the planted flips."""
+    free, _ = torch.cuda.mem_get_info(dev)
+    fit = int(free * 0.85) // (L + 5) // 1_000_000 * 1_000_000
+    n_ref = min(total, fit)
+    if n_ref <= 0:
+        return {"skipped": f"no room on rank 0's GPU ({free} B free)"}
+    frames = make_frames(eng, 0, n_ref, L, seed, flip_every, dev)
+    crc = torch.empty(n_ref, dtype=torch.int32, device=dev)
+    valid = torch.empty(n_ref, dtype=torch.uint8, device=dev)
+    eng.crc_fixed(frames, L, n=n_ref, crc_out=crc, valid_out=valid)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        eng.crc_fixed(frames, L, n=n_ref, crc_out=crc, valid_out=valid)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    ok = bool(np.array_equal(valid.cpu().numpy(), expected_valid(0, n_ref, flip_every)))
+    del frames, crc, valid
+    torch.cuda.empty_cache()
+    return {"value": round(n_ref * L / (ms * 1e-3) / 2**30, 2), "unit": "GiB/s", "ms_per_step": round(ms, 4),
+            "frames": n_ref, "whole_batch": n_ref == total, "valid_flags_as_planted": ok,
+            "what": f"{n_ref} x {L}-B frames of the same batch gated by rank 0's GPU alone "
+                    "(ufc_crc_batch_fixed: the N = 1 sharded path, nothing to transfer), HIP events over "
+                    f"{steps} calls, after the timed region"}
+
+
 def read_ceiling(eng, buf, stream, groups=5, per_group=10):
     """Plain read-only stream of buf (the gate's own frame buffer) timed like the gate: HIP events
     around groups of back-to-back launches.  Returns (GB/s, ms per launch, bytes per launch)."""
@@ -378,8 +411,9 @@ def main():
     gather = torch.cuda.Stream(dev) if sharded else None
     gathered = [None, None]  # event on the gather stream after each slot's last gather
     k_step = [0]
+    tails = []  # N > 1, timed steps: (compute-stream end, gather-stream end) timing events per step
 
-    def step(ev=None):
+    def step(ev=None, tail=None):
         i = k_step[0] % len(slots)
         k_step[0] += 1
         crc, valid = slots[i]
@@ -391,9 +425,13 @@ def main():
             eng.crc_fixed(frames, L, n=n, crc_out=crc, valid_out=valid)
         else:
             gate.crc_sharded(frames, L, total, crc, valid, root=0, stream=compute, gather_stream=gather)
-            e = torch.cuda.Event()
+            e = torch.cuda.Event(enable_timing=tail is not None)
             e.record(gather)
             gathered[i] = e
+            if tail is not None:
+                c_end = torch.cuda.Event(enable_timing=True)
+                c_end.record(compute)
+                tail.append((c_end, e))
         if ev is not None and ev[1] is not None:
             ev[1].record(compute)
         return i
@@ -421,7 +459,7 @@ def main():
     t0 = time.perf_counter()
     last = 0
     for i in range(a.steps):
-        last = step(evs[i])
+        last = step(evs[i], tails if sharded else None)
     torch.cuda.synchronize(dev)
     if sharded:
         dist.barrier()
@@ -433,6 +471,15 @@ def main():
         elapsed = float(t.item())
     kern_all = np.array([e0.elapsed_time(e1) / (g1 - g0) for (g0, g1), (e0, e1) in zip(groups, gev)])
     kern_ms = float(np.mean(kern_all))
+    # N > 1: every rank's gate time per step (compute stream) and how far its gather stream ran past
+    # its last gate of the step (the transfer the gate did not hide), gathered to rank 0
+    split = None
+    if sharded:
+        tail_ms = float(np.mean([max(0.0, c.elapsed_time(g)) for c, g in tails])) if tails else 0.0
+        mine = torch.tensor([kern_ms, tail_ms], dtype=torch.float64, device=dev)
+        every = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(world)]
+        dist.all_gather(every, mine)
+        split = [[float(x) for x in t.cpu()] for t in every]
 
     # ---- read-only streaming ceiling, after the timed region, on rank 0 ----
     ceiling = None
@@ -485,6 +532,15 @@ def main():
                   f"({time.perf_counter() - t_chk:.1f} s, {threads} threads per rank)")
         ok = ok and exact and all_local_ok
 
+    # N > 1: config 4's batch gated by rank 0's GPU alone (the N = 1 point of the same workload, no
+    # gather), after the timed region, every other rank waiting at the barrier: the driver's 1 -> N curve
+    # then separates the gate's scaling from the gather's cost and from the batch size.
+    n1_ref = None
+    if sharded and world > 1 and not a.no_n1_ref:
+        if rank == 0:
+            n1_ref = n1_sharded_reference(eng, total, L, seed, a.flip_every, dev)
+        dist.barrier()
+
     result = None
     if rank == 0:
         algo_bytes = n * L + n * 4 + n * 1  # per launch group: frames read + crc words + valid bytes
@@ -534,6 +590,14 @@ def main():
                 **({"traffic_source": tsrc} if tsrc else {}),
             },
         }
+        if split is not None:
+            result["per_rank_kernel_ms"] = [round(x[0], 4) for x in split]
+            result["gather_ms"] = [round(x[1], 4) for x in split]
+            result["gather_ms_meaning"] = ("per rank and step: how long its gather stream ran past its last "
+                                           "gate of the step (HIP events; the RCCL transfer the gates did not "
+                                           "hide); per_rank_kernel_ms: that rank's gates per step")
+        if n1_ref is not None:
+            result["n1_sharded_ref"] = n1_ref
         if ceiling is not None:
             gbs, probe_ms, probe_bytes = ceiling
             result["roofline"].update({

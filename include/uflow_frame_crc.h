@@ -90,25 +90,26 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 
 /* Kernel-selection options of a context (A/B measurement and tests; the defaults are the measured
  * fastest).  Results never depend on them.  Set between calls, not while work is queued.  Values
- * marked (tuning) select kernels measured slower than the default; they exist only in -DUFC_TUNING
- * builds of the library, and ufc_ctx_set_option rejects them (UFC_ERR_INVALID_ARG) in the product. */
+ * marked (removed) name kernels of earlier rounds that were measured slower and deleted;
+ * ufc_ctx_set_option rejects them (UFC_ERR_INVALID_ARG).  Numbers are never reused. */
 #define UFC_OPT_FIXED_KERNEL 0   /* fixed-stride batches: */
 #define UFC_FIXED_AUTO 0         /*   lean kernel when eligible (default) */
 #define UFC_FIXED_GENERIC 1      /*   the generic kernel */
-#define UFC_FIXED_CLAIM16 2      /*   (tuning) lean kernel, claimed schedule at 16 waves (round-1 default) */
+#define UFC_FIXED_CLAIM16 2      /*   (removed) lean kernel, claimed schedule at 16 waves (round-1 default) */
 #define UFC_OPT_VARLEN_KERNEL 1  /* CSR / pairs batches: */
 #define UFC_VARLEN_AUTO 0        /*   the default: UFC_VARLEN_SORTED8 */
-#define UFC_VARLEN_GENERIC 1     /*   the generic kernel */
-#define UFC_VARLEN_SORTED 2      /*   (tuning) round-1 kernel on frames sorted by block count within runs of 64 */
-#define UFC_VARLEN_BLOCKED8 3    /*   (tuning) round-1 kernel, static blocked schedule at 8 waves */
-#define UFC_VARLEN_CLAIM16 4     /*   (tuning) round-1 kernel, claimed sets at 16 waves (round-1 default) */
-#define UFC_VARLEN_BLOCKSTREAM 5 /*   (removed in round 4, rejected: the block-stream kernel, measured slower) */
+#define UFC_VARLEN_GENERIC 1     /*   the generic kernel (CSR only; pairs take the default) */
+#define UFC_VARLEN_SORTED 2      /*   (removed) round-1 kernel on frames sorted by block count within runs of 64 */
+#define UFC_VARLEN_BLOCKED8 3    /*   (removed) round-1 kernel, static blocked schedule at 8 waves */
+#define UFC_VARLEN_CLAIM16 4     /*   (removed) round-1 kernel, claimed sets at 16 waves (round-1 default) */
+#define UFC_VARLEN_BLOCKSTREAM 5 /*   (removed) the block-stream kernel */
 #define UFC_VARLEN_SORTED8 6     /*   runs of 64 sorted in the kernel, 8-frame sets of 8 lanes per frame */
-#define UFC_VARLEN_STREAM 7      /*   (removed in round 4, rejected: the byte-balanced stream kernel, measured slower) */
+#define UFC_VARLEN_STREAM 7      /*   (removed) the byte-balanced stream kernel */
 #define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
 #define UFC_OPT_SEAL_KERNEL 3    /* fixed-stride seals: */
-#define UFC_SEAL_INLINE 0        /*   the CRC kernel writes each workgroup's trailers after its reads (default) */
-#define UFC_SEAL_TWO_PASS 1      /*   validate kernel's CRC words, then a non-temporal trailer pass (round-3 default) */
+#define UFC_SEAL_TWO_PASS 0      /*   validate kernel's CRC words, then a non-temporal trailer pass (the round-3 default) */
+#define UFC_SEAL_INLINE 1        /*   the CRC kernel writes each workgroup's trailers after its reads (the default
+                                  *   since round 4: ufc_ctx_create sets it) */
 #define UFC_OPT_COUNT_ 4
 int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value);
 int ufc_ctx_get_option(const ufc_ctx* ctx, int option);
@@ -217,7 +218,13 @@ int ufc_shard_gather_plan(const uint64_t* bounds, int nranks, int rank, int root
 int ufc_comm_id_create(uint8_t id[UFC_COMM_ID_BYTES]);
 /* Collective over the nranks processes (one per GPU, each with its own ufc_ctx). */
 int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const uint8_t id[UFC_COMM_ID_BYTES]);
+/* UFC_ERR_COMM for a stalled communicator (see ufc_comm_set_timeout): its RCCL state is left to
+ * process exit, the handle is freed. */
 int ufc_comm_destroy(ufc_comm* comm);
+/* How long a sharded call waits for every peer to join it (its status agreement, see ufc_crc_sharded),
+ * in ms; 0 = for ever; default 60000.  Replaces the caller-side supervision a plain RCCL collective
+ * needs (server/mod.rs:591-602's loop cannot wait for ever on a dead peer). */
+int ufc_comm_set_timeout(ufc_comm* comm, int timeout_ms);
 /* Last RCCL result code seen by this communicator (0 if none). */
 int ufc_comm_last_error(const ufc_comm* comm);
 /* Collective: the batched gate on this rank's shard, then the gather to `root`.
@@ -234,13 +241,16 @@ int ufc_comm_last_error(const ufc_comm* comm);
  * rank sees alike are checked before any transfer, so a bad call fails on every rank.  Arguments
  * only this rank can check (its shard pointers) are agreed before any transfer with a one-word
  * all-reduce on a second communicator: a rank that rejects its part returns UFC_ERR_INVALID_ARG,
- * every other rank UFC_ERR_PEER, nothing is queued and the communicator stays usable.  Like any RCCL
- * collective, the call waits for every peer to make it: a peer that never does (crashed, or calling
- * something else) is the caller's job supervision to detect (there is no deadline: ncclCommAbort
- * measured not to return while the peer has not joined, on the socket transport).  A failure that only this rank sees after the gather has begun (a HIP launch
- * error) aborts the communicator (ncclCommAbort) and marks it unusable (later calls return
- * UFC_ERR_COMM): the peers' transfers then fail or stall, and the caller must tear down every
- * rank's communicator. */
+ * every other rank UFC_ERR_PEER, nothing is queued and the communicator stays usable.  That
+ * agreement blocks the calling host thread until every peer has made the call: a sharded call is
+ * asynchronous on `stream` only from then on.  A peer that has not made it within the communicator's
+ * deadline (ufc_comm_set_timeout; crashed, or calling something else) fails the call with
+ * UFC_ERR_COMM without aborting anything (ncclCommAbort measured not to return while the peer has not
+ * joined, on the socket transport): the communicator is then stalled, every later call returns
+ * UFC_ERR_COMM, and the caller should end the process with an error.  A failure that only this rank
+ * sees after the gather has begun (a HIP launch error) aborts the communicator (ncclCommAbort) and
+ * marks it unusable (later calls return UFC_ERR_COMM): the peers' transfers then fail or stall, and
+ * the caller must tear down every rank's communicator. */
 int ufc_crc_sharded(ufc_comm* comm, const uint8_t* d_frames, size_t stride, size_t frame_len, uint64_t n_total,
                     uint32_t* d_crc_out, uint8_t* d_valid_out, int root, void* stream, void* gather_stream);
 /* Variable-length form: rank r's shard is the frames [bounds[r], bounds[r+1]) (ufc_shard_bounds_varlen

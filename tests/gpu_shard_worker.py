@@ -9,10 +9,17 @@ gathered CRC word and valid flag against the CPU oracle over the whole batch and
 Then a rank-local failure: the last rank passes no shard (NULL frames); every rank must return an
 error (that rank UFC_ERR_INVALID_ARG, the others UFC_ERR_PEER) instead of hanging, and the next call
 on the same communicator must succeed.
+
+--peer-timeout (world 2): a peer that never makes the call.  Rank 1 creates the communicator and then
+never calls ufc_crc_sharded; rank 0 calls it with a 3-s deadline (ufc_comm_set_timeout), must get
+UFC_ERR_COMM within the deadline instead of hanging, then UFC_ERR_COMM at once from the stalled
+communicator, prints what it saw and exits with status 3 (os._exit: the pending all-reduce is left to
+process exit); rank 1 leaves once rank 0 has answered.
 """
 import json
 import os
 import sys
+import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -31,6 +38,44 @@ import oracle  # noqa: E402
 from uflow_amd import synth  # noqa: E402
 from uflow_amd.batch import FrameCrcEngine  # noqa: E402
 from uflow_amd.shard import ShardedGate, comm_id_create, shard_bounds_fixed, shard_bounds_varlen  # noqa: E402
+
+
+def peer_timeout():
+    from uflow_amd._native import UFC_ERR_COMM, NativeError
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    eng = FrameCrcEngine(0)
+    idt = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        idt.copy_(torch.frombuffer(bytearray(comm_id_create()), dtype=torch.uint8))
+    dist.broadcast(idt, src=0)
+    gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
+    torch.cuda.synchronize()
+    flag = os.path.join("/tmp", "ufc_peer_timeout_%s.done" % os.environ["MASTER_PORT"])
+    if rank != 0:  # the peer that never calls: wait for rank 0's verdict, then leave
+        t0 = time.monotonic()
+        while not os.path.exists(flag) and time.monotonic() - t0 < 90:
+            time.sleep(0.1)
+        os._exit(0)
+    total, L = 100_000, 64
+    b = shard_bounds_fixed(total, world)
+    frames = synth.fixed_frames(int(b[1] - b[0]), L, synth.SEED_CONFIG4, device=dev)
+    crc = torch.full((total,), -1, dtype=torch.int32, device=dev)
+    gate.set_timeout(3000)
+    codes = []
+    t0 = time.monotonic()
+    for _ in range(2):
+        try:
+            gate.crc_sharded(frames, L, total, crc, None, root=0)
+            codes.append(0)
+        except NativeError as e:
+            codes.append(e.code)
+        codes.append(round(time.monotonic() - t0, 3))
+    print(json.dumps({"peer_timeout_codes": codes, "UFC_ERR_COMM": UFC_ERR_COMM}), flush=True)
+    with open(flag, "w") as f:
+        f.write("done")
+    os._exit(3 if codes[0] == UFC_ERR_COMM else 4)
 
 
 def main():
@@ -129,4 +174,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if "--peer-timeout" in sys.argv:
+        peer_timeout()
+    else:
+        main()

@@ -56,3 +56,8 @@ def test_bench_two_ranks_one_device():
     assert "oracle valid flags == planted flips on every rank: True" in j["data"]
     assert "valid flags as planted: True" in j["data"]
     assert j["cpu_baseline"]["value"] > 0 and j["roofline"]["ceiling_GBs"] > 0
+    # the N > 1 line separates the gates from the gather
+    assert len(j["per_rank_kernel_ms"]) == 2 and all(x > 0 for x in j["per_rank_kernel_ms"])
+    assert len(j["gather_ms"]) == 2 and all(x >= 0 for x in j["gather_ms"])
+    ref = j["n1_sharded_ref"]
+    assert ref["value"] > 0 and ref["frames"] > 0 and ref["valid_flags_as_planted"]

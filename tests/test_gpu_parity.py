@@ -616,9 +616,9 @@ def test_fixed_multi_launch(engine, frame_len, extra):
         assert np.array_equal(got, ref_crc)
 
 
-def test_tuning_only_modes_rejected(engine):
-    """Kernels measured slower than the defaults exist only in -DUFC_TUNING builds: the product
-    library refuses to select them (include/uflow_frame_crc.h, "(tuning)")."""
+def test_removed_modes_rejected(engine):
+    """Kernels of earlier rounds measured slower than the defaults were deleted: the library refuses
+    to select them (include/uflow_frame_crc.h, "(removed)")."""
     from uflow_amd import _native as N
     for opt, val in ((N.UFC_OPT_FIXED_KERNEL, N.UFC_FIXED_CLAIM16), (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_SORTED),
                      (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_BLOCKED8), (N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_CLAIM16),

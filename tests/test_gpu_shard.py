@@ -160,3 +160,20 @@ def test_ranks_on_one_device(world):
     # (-6), nobody hangs, and the next call on the same communicators is exact
     assert j["fail_codes"] == [-6] * (world - 1) + [-1]
     assert j["after_fail_crc_ok"]
+
+
+def test_sharded_peer_timeout():
+    """A peer that never makes the call: rank 1 of 2 (both on cuda:0) creates the
+    communicator and never calls ufc_crc_sharded; rank 0, with a 3-s deadline, gets UFC_ERR_COMM within
+    it instead of hanging (no ncclCommAbort), then UFC_ERR_COMM at once from the stalled communicator,
+    and exits non-zero (tests/gpu_shard_worker.py --peer-timeout).  Reference caller:
+    /root/reference/src/server/mod.rs:591-602 (a receive loop that must not wait for ever)."""
+    p = _run_worker(2, ["--peer-timeout"], 120)
+    objs = re.findall(r"\{[^{}]*\}", p.stdout)
+    assert len(objs) == 1, (p.stdout[-2000:], p.stderr[-2000:])
+    j = json.loads(objs[0])
+    code0, t0, code1, t1 = j["peer_timeout_codes"]
+    assert code0 == j["UFC_ERR_COMM"] and code1 == j["UFC_ERR_COMM"], j
+    assert 2.5 <= t0 <= 30.0, j   # the deadline, not a hang
+    assert t1 - t0 < 1.0, j       # a stalled communicator fails at once
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])

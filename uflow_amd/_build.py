@@ -11,10 +11,8 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 LIB_PATH = os.path.join(PKG_DIR, "libuflowcrc.so")
-SOURCES = ["frame_crc.hip", "frame_crc_varlen.hip", "frame_crc_varlen8.hip", "frame_parse.hip", "hbm_probe.hip",
+SOURCES = ["frame_crc.hip", "frame_crc_varlen8.hip", "frame_parse.hip", "hbm_probe.hip",
            "ufc_api.cpp", "ufc_shard.cpp", "crc_math.cpp", "frame_codec.cpp"]
-# Kernels measured slower than the product's, kept for A/B in tuning builds only.
-TUNING_SOURCES = []
 HEADERS = ["frame_crc_dev.hpp", "frame_crc_kernels.hpp", "crc_math.hpp", "frame_codec_core.hpp", "frame_parse.hpp",
            "ufc_internal.hpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
@@ -60,35 +58,27 @@ def _stamp_defines(target):
     return tuple(line[len("defines:"):].split()) if line.startswith("defines:") else ()
 
 
-def _native_identity(tuning=False, defines=()):
+def _native_identity(defines=()):
     """(sources, hipcc flags, digest) of a native build from the sources in this tree."""
-    sources = SOURCES + (TUNING_SOURCES if tuning else [])
+    sources = list(SOURCES)
     deps = [os.path.join(CSRC, s) for s in sources + HEADERS]
     deps += [os.path.join(REPO_DIR, "include", h) for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
     # No atomic optimizer: the lean kernel's single-lane claim atomics must stay plain
     # global_atomic_add (the optimizer reads the result back at once, forcing a vmcnt(0) wait).
     flags = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall",
              "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
-    if tuning:
-        flags.append("-DUFC_TUNING")
     flags += ["-D" + d for d in defines]
     return sources, flags, _digest(deps + [os.path.abspath(__file__)], flags[1:])
 
 
-def tuning_lib_current(path):
-    """Whether the tuning library at `path` was built from this tree's sources (its stamp), with the
-    -D defines its stamp records (ablation builds)."""
-    return _stamp_ok(path, _native_identity(tuning=True, defines=_stamp_defines(path))[2])
-
-
-def build_native(force=False, verbose=False, tuning=False, out=None, defines=()):
-    """tuning=True adds the ablation kernels (-DUFC_TUNING); `defines` adds -D flags (tuning
-    experiments).  Both are meant with `out` pointing away from the product library.
+def build_native(force=False, verbose=False, out=None, defines=()):
+    """`defines` adds -D flags (an experiment build, meant with `out` pointing away from the product
+    library).
 
     Rebuilds when the sha256 of the sources, headers, flags and this file differs from the one
     recorded beside the library (<lib>.sha256), not by file times: a library copied to another
     machine (the GPU box) with its stamp is rebuilt there only if it does not match the source."""
-    sources, flags, digest = _native_identity(tuning, defines)
+    sources, flags, digest = _native_identity(defines)
     target = out or LIB_PATH
     if not force and _stamp_ok(target, digest):
         return target

@@ -10,13 +10,9 @@ import os
 
 from ._build import LIB_PATH as _DEFAULT_LIB
 
-# UFC_LIB overrides the library path (tuning builds only; the product loads the in-tree .so).
+# UFC_LIB overrides the library path (A/B measurement against another build; the product loads the
+# in-tree .so).
 LIB_PATH = os.environ.get("UFC_LIB", _DEFAULT_LIB)
-if os.path.basename(LIB_PATH).startswith("libuflowcrc_tuning") and os.environ.get("UFC_LIB_ANY") != "1":
-    from ._build import tuning_lib_current as _current
-    if not _current(LIB_PATH):  # (an A/B against a stale tuning build measures old code)
-        raise RuntimeError(f"{LIB_PATH} was not built from this tree's sources: rebuild it with "
-                           "build_native(tuning=True, out=...) (or set UFC_LIB_ANY=1)")
 
 UFC_OK = 0
 UFC_ERR_INVALID_ARG = -1
@@ -34,7 +30,7 @@ UFC_OPT_FIXED_KERNEL, UFC_OPT_VARLEN_KERNEL, UFC_OPT_GENERIC_JC = 0, 1, 2
 UFC_FIXED_AUTO, UFC_FIXED_GENERIC, UFC_FIXED_CLAIM16 = 0, 1, 2
 UFC_VARLEN_AUTO, UFC_VARLEN_GENERIC, UFC_VARLEN_SORTED, UFC_VARLEN_BLOCKED8, UFC_VARLEN_CLAIM16 = 0, 1, 2, 3, 4
 UFC_VARLEN_BLOCKSTREAM, UFC_VARLEN_SORTED8, UFC_VARLEN_STREAM = 5, 6, 7
-UFC_OPT_SEAL_KERNEL, UFC_SEAL_INLINE, UFC_SEAL_TWO_PASS = 3, 0, 1
+UFC_OPT_SEAL_KERNEL, UFC_SEAL_INLINE, UFC_SEAL_TWO_PASS = 3, 1, 0
 
 # Every symbol the header declares, with its ctypes signature.
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -87,6 +83,7 @@ _SIGNATURES = {
                                        ctypes.c_void_p]),
     "ufc_comm_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "ufc_comm_last_error": (ctypes.c_int, [ctypes.c_void_p]),
+    "ufc_comm_set_timeout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "ufc_crc_sharded": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64,
                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "ufc_crc_sharded_varlen": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

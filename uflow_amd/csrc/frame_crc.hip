@@ -377,9 +377,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   constexpr bool ILV = SCHED == kSchedInterleave;   // static: wave i takes lo + i + k * WAVES
   constexpr uint32_t kInc = ILV ? (uint32_t)WAVES : 1u;  // step of a static sequence
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-#ifdef UFC_TUNING
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-#endif
   const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
   Lane L;
   init_lane(L, lds, p.G);
@@ -640,9 +637,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
     load(q_cur, A);
   if (DEPTH == 3) load(q_nx1, B);
   stage_store<WAVES * 64>(sr, lds);
-#ifdef UFC_TUNING
-  const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
-#endif
   q_nx2 = (DEPTH == 3 && !DYN) ? q_cur + 2 * kInc : 0;
 
   // Edge sets [0, s_fast) (the first sets of the batch only): global wave 0, before its main
@@ -837,17 +831,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       __hip_atomic_store(ctr + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-#ifdef UFC_TUNING
-  if (p.dbg && L.lane == 0) {
-    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-    unsigned long long* d = p.dbg + 4 * w;
-    d[0] = t_start;
-    d[1] = t_staged;
-    d[2] = t_end;
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
-    d[3] = (unsigned long long)(q_end - q_lo) | ((unsigned long long)__smid() << 32) | ((unsigned long long)xcc << 56);
-  }
-#endif
 }
 
 // Product configuration: interleaved schedule, 8 waves, depth 2 (measured fastest, DESIGN.md
@@ -858,59 +841,6 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   template __global__ void frame_crc_fixed_kernel<J, true, 2, 0, kSchedInterleave, 8>(const KernelParams);
 UFC_INST_FIXED(1) UFC_INST_FIXED(2) UFC_INST_FIXED(3) UFC_INST_FIXED(4) UFC_INST_FIXED(5) UFC_INST_FIXED(6)
 
-#ifdef UFC_TUNING
-// Loads-only streaming probe over a fixed-length batch (tuning builds only): the lean kernel's
-// lane->address pattern (4 frames per wave-instruction, 256-B runs right-aligned to the frame end),
-// static interleaved schedule, NBUF sets in flight per wave, no LDS (STAGE: the lean kernel's LDS
-// table staging first).  Results are meaningless (an XOR fold per lane lands in crc_out).
-// ALIGN (bytes, 0 = none): each frame's window start rounded down to ALIGN (the same J x 256 bytes
-// read per frame), to measure what unaligned 256-byte pieces cost the memory pipeline.
-template <int NBUF, int WAVES, bool STAGE, int ALIGN = 0>
-__global__ __launch_bounds__(WAVES * 64) void fixed_probe_kernel(const KernelParams p) {
-  __shared__ __attribute__((aligned(16))) char lds[STAGE ? kLdsBytes : 16];
-  constexpr int NI = 6;
-  if (STAGE) {
-    const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
-    stage_store<WAVES * 64>(sr, lds);
-  }
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nsets = (int)(p.nframes / 4);
-  const int lo = (int)((int64_t)nsets * blockIdx.x / gridDim.x);
-  const int hi = (int)((int64_t)nsets * (blockIdx.x + 1) / gridDim.x);
-  const int64_t stride = (int64_t)p.stride;
-  uint32_t acc = 0;
-  uint4 buf[NBUF][NI];
-  auto load = [&](int q, uint4 (&x)[NI]) {
-    const int qc = min(q, nsets - 1);
-    const int f = lane >> 4, col = lane & 15;
-    int64_t w0 = (int64_t)qc * 4 * stride + f * stride - (NI * 256 - (int64_t)p.frame_len);
-    if (ALIGN) w0 = w0 & ~(int64_t)(ALIGN - 1);
-    int64_t off = w0 + 16 * col;
-    off = off < 0 ? 0 : off;
-#pragma unroll
-    for (int j = 0; j < NI; j++) {
-      const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(p.bytes + off + 256 * j));
-      x[j] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-  };
-  int q = lo + wid;
-#pragma unroll
-  for (int b = 0; b < NBUF - 1; b++) load(q + WAVES * b, buf[b]);
-  for (; q < hi; q += WAVES * NBUF) {
-#pragma unroll
-    for (int b = 0; b < NBUF; b++) {
-      load(q + WAVES * (b + NBUF - 1), buf[(b + NBUF - 1) % NBUF]);
-      if (q + WAVES * b < hi) {
-#pragma unroll
-        for (int j = 0; j < NI; j++) acc ^= buf[b][j].x ^ buf[b][j].y ^ buf[b][j].z ^ buf[b][j].w;
-      }
-    }
-  }
-  if (STAGE) acc ^= *(const uint32_t*)(lds + 4 * (threadIdx.x & 31));
-  if (p.crc_out) p.crc_out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
-}
-#endif
 
 const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves) {
   if (abl == 0 && depth == 2 && sched == kSchedInterleave && waves == 8) {  // the product kernel
@@ -924,65 +854,6 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
       default: return nullptr;
     }
   }
-#ifdef UFC_TUNING
-  // Round-1 default (claimed schedule, 16 waves, depth 3): measured slower, A/B builds only.
-  if (abl == 0 && depth == 3 && sched == kSchedClaim && waves == 16 && J >= 1 && J <= 6) {
-    static const void* const t16[6][2] = {
-#define UFC_C16(JJ) {(const void*)frame_crc_fixed_kernel<JJ, false, 3, 0, kSchedClaim, 16>, \
-                     (const void*)frame_crc_fixed_kernel<JJ, true, 3, 0, kSchedClaim, 16>}
-        UFC_C16(1), UFC_C16(2), UFC_C16(3), UFC_C16(4), UFC_C16(5), UFC_C16(6)};
-#undef UFC_C16
-    return t16[J - 1][seal ? 1 : 0];
-  }
-  if (J == 6 && !seal && abl >= 3 && abl <= 4 && (depth == 2 || depth == 3)) {  // loads-only probes
-    static const void* const ptab[2][2][2] = {  // [waves 8/16][stage][nbuf 2/3]
-        {{(const void*)fixed_probe_kernel<2, 8, false>, (const void*)fixed_probe_kernel<3, 8, false>},
-         {(const void*)fixed_probe_kernel<2, 8, true>, (const void*)fixed_probe_kernel<3, 8, true>}},
-        {{(const void*)fixed_probe_kernel<2, 16, false>, (const void*)fixed_probe_kernel<3, 16, false>},
-         {(const void*)fixed_probe_kernel<2, 16, true>, (const void*)fixed_probe_kernel<3, 16, true>}}};
-    return ptab[waves == 16][abl == 4][depth - 2];
-  }
-  if (J == 6 && !seal && abl >= 6 && abl <= 8)  // loads-only probe, staged tables, 2 sets: aligned windows
-    return abl == 6 ? (const void*)fixed_probe_kernel<2, 8, true, 64>
-                    : abl == 7 ? (const void*)fixed_probe_kernel<2, 8, true, 128>
-                               : (const void*)fixed_probe_kernel<2, 8, true, 256>;
-  if (J == 6 && !seal && depth == 1 && sched == kSchedInterleave && (abl == 0 || abl == 1)) {
-    if (waves == 8)
-      return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 8>
-                      : (const void*)frame_crc_fixed_kernel<6, false, 1, kLeanAblLoads, kSchedInterleave, 8>;
-    return abl == 0 ? (const void*)frame_crc_fixed_kernel<6, false, 1, 0, kSchedInterleave, 16>
-                    : (const void*)frame_crc_fixed_kernel<6, false, 1, kLeanAblLoads, kSchedInterleave, 16>;
-  }
-  if (J == 6 && depth == 2 && waves == 8 && sched == kSchedInterleave && abl >= 100000) {  // LOADV = abl - 100000
-    switch (abl - 100000) {
-#define UFC_LV(V)                                                                          \
-  case V:                                                                                  \
-    return seal ? (const void*)frame_crc_fixed_kernel<6, true, 2, 0, kSchedInterleave, 8, V> \
-                : (const void*)frame_crc_fixed_kernel<6, false, 2, 0, kSchedInterleave, 8, V>;
-      UFC_LV(kLoadvAllNT) UFC_LV(lean_loadv(0, 0, 2, 0)) UFC_LV(lean_loadv(0, 2, 2, 0))
-      UFC_LV(lean_loadv(0, 0, 18, 18)) UFC_LV(lean_loadv(0, 0, 3, 3)) UFC_LV(lean_loadv(0, 1, 2, 2))
-      UFC_LV(lean_loadv(0, 16, 2, 2)) UFC_LV(lean_loadv(1, 0, 2, 2)) UFC_LV(lean_loadv(0, 0, 18, 2))
-      UFC_LV(lean_loadv(0, 0, 2, 18)) UFC_LV(lean_loadv(0, 0, 0, 2))
-#undef UFC_LV
-      default: return nullptr;
-    }
-  }
-  if (J == 6 && !seal && depth == 2 && waves == 8 && sched == kSchedInterleave && abl == 5)
-    return (const void*)frame_crc_fixed_kernel<6, false, 2, 5, kSchedInterleave, 8>;
-  if (J == 6 && !seal && (depth == 2 || depth == 3) && abl >= 0 && abl <= 2 && sched >= 0 && sched <= 2) {
-    // A/B variants (J = 6, validate), instantiated by taking their addresses here.
-    static const void* const tab[2][3][3][2] = {  // [waves 8/16][sched][abl][depth 2/3]
-#define UFC_T(WV, SC, AB) {(const void*)frame_crc_fixed_kernel<6, false, 2, AB, SC, WV>, \
-                           (const void*)frame_crc_fixed_kernel<6, false, 3, AB, SC, WV>}
-#define UFC_TS(WV, SC) {UFC_T(WV, SC, 0), UFC_T(WV, SC, kLeanAblLoads), UFC_T(WV, SC, kLeanAblCompute)}
-#define UFC_TW(WV) {UFC_TS(WV, kSchedRange), UFC_TS(WV, kSchedClaim), UFC_TS(WV, kSchedInterleave)}
-        UFC_TW(8), UFC_TW(16)};
-#undef UFC_TW
-#undef UFC_TS
-#undef UFC_T
-    return tab[waves == 16][sched][abl][depth - 2];
-  }
-#endif
   return nullptr;
 }
 
@@ -998,10 +869,6 @@ const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched,
 
 UFC_CONFIGS(UFC_INST_MODES)
 
-#ifdef UFC_TUNING
-template __global__ void frame_crc_kernel<6, kModeAblateCompute>(const KernelParams);
-template __global__ void frame_crc_kernel<6, kModeAblateLoads>(const KernelParams);
-#endif
 
 const void* kernel_symbol(int jc, int mode) {
 #define UFC_PICK(JC)                                                                                   \
@@ -1018,10 +885,6 @@ const void* kernel_symbol(int jc, int mode) {
   }
   UFC_CONFIGS(UFC_PICK)
 #undef UFC_PICK
-#ifdef UFC_TUNING
-  if (jc == 6 && mode == kModeAblateCompute) return (const void*)frame_crc_kernel<6, kModeAblateCompute>;
-  if (jc == 6 && mode == kModeAblateLoads) return (const void*)frame_crc_kernel<6, kModeAblateLoads>;
-#endif
   return nullptr;
 }
 

@@ -114,13 +114,17 @@ __device__ __forceinline__ uint32_t row_xor16(uint32_t v) {
   return v;
 }
 
+// ---- Mask and shift helpers (host and device: tests/c/ubsan_helpers.hip drives every one of them over
+// its whole argument range as host code under UBSan).  Every variable shift amount is kept in range
+// in every arm, selected or not.
+
 // Word of the virtual stream whose first byte sits at frame offset o (o < 0: before the frame).
 // Bytes at frame offsets [-4, 0) are G's bytes, below -4 zeros, from 0 on the loaded data v.
-__device__ __forceinline__ uint32_t fix_word(uint32_t v, int o, uint32_t G) {
+__host__ __device__ __forceinline__ uint32_t fix_word(uint32_t v, int o, uint32_t G) {
   const uint64_t pv = (uint64_t)G << 32;
-  const int sh = 8 * (o + 8);  // in [8, 56] when o in (-8, 0)
-  const uint32_t pre = (uint32_t)(pv >> (sh & 63));
-  const uint32_t dm = (o > -4) ? (0xFFFFFFFFu << ((8 * (-o)) & 31)) : 0u;
+  const uint32_t sh = (uint32_t)(8 * (o + 8)) & 63u;  // in [8, 56] when o in (-8, 0)
+  const uint32_t pre = (uint32_t)(pv >> sh);
+  const uint32_t dm = (o > -4 && o < 0) ? (0xFFFFFFFFu << ((uint32_t)(-8 * o) & 31u)) : 0u;
   const uint32_t mixed = (v & dm) | (pre & ~dm);
   return (o >= 0) ? v : ((o <= -8) ? 0u : mixed);
 }
@@ -128,12 +132,10 @@ __device__ __forceinline__ uint32_t fix_word(uint32_t v, int o, uint32_t G) {
 // Block 0 of a frame, lane with p = pad - 16 col bytes before the frame: bytes before the frame
 // become zeros, except the 4 right before it, which become G (the reference's initial ~0 folded
 // into a linear CRC).  p <= 0: the data unchanged; p >= 20: all zero.
-__device__ __forceinline__ uint4 front_fix(uint4 x, int p, uint32_t G) {
-  const uint32_t pc = (uint32_t)min(max(p, 0), 20);
+__host__ __device__ __forceinline__ uint4 front_fix(uint4 x, int p, uint32_t G) {
+  const uint32_t pc = (uint32_t)(p < 0 ? 0 : (p > 20 ? 20 : p));
   const uint32_t s = 8u * pc;  // data bytes start at bit s of the 128-bit lane
   const uint64_t lo = (uint64_t)x.x | ((uint64_t)x.y << 32), hi = (uint64_t)x.z | ((uint64_t)x.w << 32);
-  // (every shift amount masked into range, also in the arms a ternary does not select: an out-of-range
-  // amount there is poison the compiler may propagate)
   const uint64_t mlo = s >= 64u ? 0ull : ~0ull << (s & 63u);
   const uint64_t mhi = s >= 128u ? 0ull : (s <= 64u ? ~0ull : ~0ull << ((s - 64u) & 63u));
   const int q = (int)pc - 4;  // G's first byte in the lane: -4..16
@@ -145,6 +147,31 @@ __device__ __forceinline__ uint4 front_fix(uint4 x, int p, uint32_t G) {
                                        : (q < 16 ? g << ((uint32_t)(8 * (q - 8)) & 63u) : 0ull));
   const uint64_t rlo = (lo & mlo) | glo, rhi = (hi & mhi) | ghi;
   return make_uint4((uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi, (uint32_t)(rhi >> 32));
+}
+
+// Byte mask of a word with lb of its bytes before the end of the CRC'd data (lb >= 4: all, <= 0: none).
+__host__ __device__ __forceinline__ uint32_t data_mask(int lb) {
+  return lb >= 4 ? 0xFFFFFFFFu : (lb > 0 ? 0xFFFFFFFFu >> ((uint32_t)(32 - 8 * lb) & 31u) : 0u);
+}
+
+// Byte mask of the word whose first byte sits at frame offset ob, for a frame of len bytes: the
+// word's bytes at offsets [0, len).
+__host__ __device__ __forceinline__ uint32_t frame_word_mask(int ob, uint32_t len) {
+  const int lo = -ob < 0 ? 0 : (-ob > 4 ? 4 : -ob);  // bytes before the frame
+  const int64_t h = (int64_t)len - ob;
+  const int hi = h < 0 ? 0 : (h > 4 ? 4 : (int)h);    // bytes before the frame's end
+  const uint32_t mhi = hi >= 4 ? ~0u : ((1u << ((uint32_t)(8 * hi) & 31u)) - 1u),
+                 mlo = lo >= 4 ? 0u : (~0u << ((uint32_t)(8 * lo) & 31u));
+  return mhi & mlo;
+}
+
+// The nibble-table key of the 8-lane finish with the slot constants rotated for a stream whose last
+// word is slot e (frame_crc_varlen8.hip, group_lin8_rot): byte i = 4 * column multiplied in nibble
+// step i, column = (4 col + ((i + u) & 3) + 31 - e) & 31 with u = (rot - (31 - e)) & 3.
+__host__ __device__ __forceinline__ uint32_t rot_nibble_key(uint32_t col, uint32_t u, uint32_t e) {
+  const uint32_t R = 31u - (e & 31u), sh = (8u * u) & 31u;
+  const uint32_t steps = (0x03020100u >> sh) | (0x03020100u << ((32u - sh) & 31u));  // byte i = (i + u) & 3
+  return ((steps + (4u * (col & 7u) + R) * 0x01010101u) & 0x1F1F1F1Fu) << 2;
 }
 
 // Per-frame description for one 16-lane group.

@@ -7,9 +7,9 @@ namespace ufc_dev {
 constexpr int kModeVarlen = 1;  // frames from a CSR offsets array
 constexpr int kModeSeal = 2;    // write the BE32 trailer instead of validating it
 constexpr int kModeFreeze = 4;  // fixed-length frames whose block count is not a multiple of JC
-// Ablation modes, instantiated only in tuning builds (-DUFC_TUNING): results are meaningless.
-constexpr int kModeAblateCompute = 8;   // loads only (data XOR-folded, no CRC)
-constexpr int kModeAblateLoads = 16;    // CRC compute on register data, no loads after the first item
+// (mode bits 8 and 16 were ablation variants of measurement builds; no kernel instantiates them)
+constexpr int kModeAblateCompute = 8;
+constexpr int kModeAblateLoads = 16;
 
 constexpr int kBlockThreads = 1024;          // one workgroup per CU, 16 waves
 constexpr int kLdsBytes = 131072 + 32768;    // chain tables + nibble tables
@@ -28,8 +28,6 @@ struct KernelParams {
   uint32_t G;                 // A^-4(~0)
   uint32_t* ctr;              // lean fixed kernel: per-workgroup claim counters (zero at launch)
   uint32_t front_ok;          // lean fixed kernel: the pad bytes before frame 0 are readable
-  unsigned long long* dbg;    // tuning builds only: per-wave timestamps (nullptr in product use)
-  const uint64_t* offsets_csr;  // varlen sorted mode: the caller's CSR offsets (n+1), or nullptr for pairs
 };
 
 // Kernel entry for (JC 256-byte blocks per pipelined part, mode); nullptr if not instantiated.
@@ -37,46 +35,29 @@ const void* kernel_symbol(int jc, int mode);
 bool config_available(int jc);
 // Lean fixed-length kernel (frame_len >= 4, J = ceil((frame_len + 4) / 256) in 1..6); one
 // workgroup per CU owning a contiguous range of 4-frame sets, spread over its waves by `sched`;
-// `depth` (2 or 3) sets in flight per wave.  Product default: interleaved, 8 waves, depth 2.
-// abl != 0 selects the ablation variants and loads-only probes of tuning builds (J = 6 only).
+// `depth` sets in flight per wave.  Only the product configuration is instantiated (interleaved,
+// 8 waves, depth 2, abl 0); other arguments return nullptr.
 constexpr int kLeanDepthDefault = 2;
 // Results stay in registers until a wave's range is done: at most 16 * kLeanRuns sets per wave,
 // i.e. a launch covers at most (waves in the grid) * 16 * kLeanRuns * 4 frames (host-chunked).
 constexpr int kLeanRuns = 8;
 // Runs of history per wave by wave count: 32 at 8 waves, kLeanRuns at 16 (register budget).
 constexpr int lean_runs(int waves) { return waves == 8 ? 32 : kLeanRuns; }
-// waves: 16 (1024-thread workgroups) or 8 (512); one workgroup per CU either way (160 KiB LDS).
 constexpr int kLeanWavesDefault = 8;
 // Schedules of a workgroup's contiguous set range over its waves: per-wave contiguous ranges,
 // claimed one set at a time from a per-workgroup counter, or interleaved (wave i: lo + i + k*waves).
 constexpr int kSchedRange = 0;
 constexpr int kSchedClaim = 1;
 constexpr int kSchedInterleave = 2;
-constexpr int kSchedBlocked = 3;  // static: runs of 16 consecutive sets, interleaved over the waves
 constexpr int kLeanSchedDefault = kSchedInterleave;
 const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves);
-// Lean variable-length kernel (CSR offsets, any frame lengths; frames of 4..1532 B on the fast
-// path, the rest byte-wise after the main loop).  Set indices are 30-bit: a launch covers fewer
-// than 2^32 frames (host-chunked).
-// pairs: frames given as (start, end) pairs instead of CSR offsets (KernelParams::offsets holds
-// 2n words, frame_len the buffer length).  abl != 0: ablation variants of tuning builds.
-// sched/waves: kSchedClaim/16 (default) or kSchedBlocked/8 (A/B).  sorted: the frames come as
-// run-sorted records (sort_runs below), p.offsets = the records.
-const void* varlen_kernel_symbol(bool seal, bool pairs, int abl, int sched, int waves, bool sorted);
-// Pre-pass of the sorted varlen mode: every run of 64 consecutive frames is ordered by its
-// frames' 256-byte block counts, so the main kernel's 4-frame sets share one block count (a set
-// otherwise computes its longest frame's blocks for all four).  Record r of run R (16 B):
-// {start (u64), len (u32), index in the run (bits 0..5) | past-the-end (bit 31)}.
 constexpr int kRunFrames = 64;
-int sort_runs(const uint64_t* offsets, bool pairs, uint64_t nframes, void* records, void* stream);
-// Sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): 8-frame sets from the
-// run-sorted records (p.offsets = records, p.offsets_csr = the CSR offsets or nullptr for pairs),
-// A^128 chain tables and the 32-slot nibble image; 12 waves, 2 sets in flight per wave.  insort:
-// runs sorted inside the kernel from the CSR offsets / pairs in p.offsets (product); otherwise
-// p.offsets = sort_runs records (tuning builds only, A/B).  Pairs need the buffer below
-// 2^31 - 2^20 bytes (32-bit offsets from the buffer).
-// geor: each run's geometry computed once per frame before the sort (GEOR in frame_crc_varlen8.hip).
-const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw = 64, int aux = 0, bool geor = false);
+// Variable-length kernel with 8 lanes per frame (frame_crc_varlen8.hip): CSR offsets (p.offsets,
+// n + 1) or (start, end) pairs (p.offsets holds 2n words, p.frame_len the buffer length); each run of
+// 64 frames ordered by piece count inside the kernel; 8-frame sets; A^128 chain tables and the
+// 32-slot nibble image.  varlen8_waves(): the workgroup's waves (one workgroup per CU).
+const void* varlen8_kernel_symbol(bool seal, bool pairs);
+int varlen8_waves();
 // Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride
 // + lens[i] (ufc_validate_host_slots_async).
 int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream);

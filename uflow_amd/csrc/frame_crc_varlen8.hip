@@ -15,9 +15,9 @@
 //     gfx950 every integer VALU instruction is 4 cycles per wave and the lean varlen kernels are
 //     VALU-bound (SQ_ACTIVE_INST_VALU ~ SQ_INSTS_VALU with the SIMD busy all along): per-frame work
 //     -- geometry, loads, front fix, finish, results -- is shared by 8 frames instead of 4.
-//   * Sets come from run-sorted records (sort_runs, frame_crc_varlen.hip): a run of 64 frames is
-//     ordered by block count J, so a set's 8 frames mostly share J (one uniform block loop, no
-//     frozen chains); a set mixing block counts freezes the chains of its shorter frames.
+//   * Sets come from sorted runs: the wave that takes a run of 64 frames orders it by block count J
+//     (ballot ranks), so a set's 8 frames mostly share J (one uniform block loop, no frozen
+//     chains); a set mixing block counts freezes the chains of its shorter frames.
 //   * Windows end at the frame's end rounded up to 4 bytes, so every load is 4-byte aligned and
 //     needs no realignment: the t = 0..3 bytes past the frame are zeroed with the trailer, which
 //     multiplies the linear CRC by A^t, undone at the finish with one nibble-table product
@@ -28,33 +28,40 @@
 //   * Results of a run (8 sets x 8 frames) collect in one register pair per lane and leave with
 //     hidden stores once per run.  Sets with a frame the fast path cannot take (shorter than 4 B,
 //     longer than 6 blocks, at the batch edges, past its end) run byte-wise, in the same loop.
+#include <type_traits>
+
 #include "frame_crc_dev.hpp"
 
 namespace ufc_dev {
 
 namespace {
 
-constexpr int kV8Blocks = 6;               // fast path: frames of 4..1532 B
-constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the set's base - bias
+constexpr int kV8Pieces = 13;              // fast path: windows of up to 13 lines (frames of 4..1532 B)
+constexpr int kV8Split = 7;                // slots 0 .. 6 in a set's first load part, 7 .. 12 and 1 in its second
+constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the run's base - bias
 constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
-constexpr int kV8Aux = 0;                  // default cache policy (shared boundary lines)
+constexpr int kV8AuxShared = 0;            // a frame's first and last line: default policy (shared)
+constexpr int kV8AuxInterior = 2;          // the lines in between: non-temporal (read once)
 constexpr uint32_t kNoSet = 0xFFFFFFFFu;   // a wave's set sequence past its last claimed run
 // The workgroup's run counter: nibble-image row 127, column 63 (columns 52..63 are never read).
 constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
 
-// Per-lane geometry of a set (one VGPR): pad [0,9), J [9,12), len >= 5 [12], t [13,15) (window
-// bytes past the frame), frame index in its run [16,22), past the batch end [22].
-__device__ __forceinline__ uint32_t v8_pad(uint32_t g) { return g & 511u; }
-__device__ __forceinline__ uint32_t v8_J(uint32_t g) { return (g >> 9) & 7u; }
-__device__ __forceinline__ uint32_t v8_t(uint32_t g) { return (g >> 13) & 3u; }
-__device__ __forceinline__ uint32_t v8_orig(uint32_t g) { return (g >> 16) & 63u; }
+// Per-lane geometry of a frame on the fast path (one VGPR): r = (frame start - 4) mod 128 [0,7) (the
+// window starts at the 128-byte line holding G's first byte, r bytes before it), len [7,18), index
+// in its run [18,24); then the set's facts, the same in every lane of the set: Pmax = its frames' most
+// lines, 0 for a byte-path set [24,28), plim = lines 0 .. plim-1 hold CRC'd data only in every frame
+// [28,32).  The trailer's first byte lies at window offset zo = len + r; lines P = ceil((zo + 4) / 128).
+__device__ __forceinline__ uint32_t w_r(uint32_t g) { return g & 127u; }
+__device__ __forceinline__ uint32_t w_len(uint32_t g) { return (g >> 7) & 2047u; }
+__device__ __forceinline__ uint32_t w_zo(uint32_t g) { return w_len(g) + w_r(g); }
+__device__ __forceinline__ uint32_t w_P(uint32_t g) { return (w_zo(g) + 131u) >> 7; }
+__device__ __forceinline__ uint32_t w_orig(uint32_t g) { return (g >> 18) & 63u; }
 
 struct Lane8 {
   const char* lds;
   uint32_t lane, col, grp;
   uint32_t K;    // chain-table key (as Lane::K)
-  uint32_t K2;   // nibble key: byte i = column*4 of the slot word multiplied in nibble step i
   uint32_t rot;  // group & 3: nibble step i multiplies slot word (i + rot) & 3
   uint32_t G;
 };
@@ -68,10 +75,6 @@ __device__ __forceinline__ void init_lane8(Lane8& L, char* lds, uint32_t G) {
   L.G = G;
   const uint32_t c4 = (L.lane & 31u) * 4u;
   L.K = c4 | ((c4 + 128u) << 8) | (1u << 24);
-  uint32_t k2 = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < 4; i++) k2 |= ((4u * L.col + ((i + L.rot) & 3u)) * 4u) << (8 * i);  // column = slot
-  L.K2 = k2;
 }
 
 // lin of the frame held by this 8-lane group (every lane of the group receives it).  The 32 lanes
@@ -80,8 +83,30 @@ __device__ __forceinline__ uint32_t group_lin8(const Lane8& L, const Chains& c) 
   const bool r1 = (L.rot & 1u) != 0, r2 = (L.rot & 2u) != 0;
   const uint32_t a01 = r1 ? c.v1 : c.v0, a12 = r1 ? c.v2 : c.v1, a23 = r1 ? c.v3 : c.v2, a30 = r1 ? c.v0 : c.v3;
   const uint32_t X0 = r2 ? a23 : a01, X1 = r2 ? a30 : a12, X2 = r2 ? a01 : a23, X3 = r2 ? a12 : a30;
-  uint32_t v = xor3(nib_mul<0>(L.lds, X0, L.K2), nib_mul<1>(L.lds, X1, L.K2), nib_mul<2>(L.lds, X2, L.K2)) ^
-               nib_mul<3>(L.lds, X3, L.K2);
+  uint32_t K2 = 0;  // byte i = column*4 of the slot word multiplied in nibble step i (column = slot)
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++) K2 |= ((4u * L.col + ((i + L.rot) & 3u)) * 4u) << (8 * i);
+  uint32_t v = xor3(nib_mul<0>(L.lds, X0, K2), nib_mul<1>(L.lds, X1, K2), nib_mul<2>(L.lds, X2, K2)) ^
+               nib_mul<3>(L.lds, X3, K2);
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return v;
+}
+
+// The same with the slot constants rotated for a stream whose last word is slot e: slot s's last
+// word then lies (e - s) mod 32 words before the stream's end, so it takes the constant of column
+// (s + 31 - e) mod 32; nibble step i multiplies slot word (i + u) & 3 with u = (group - (31 - e)) & 3,
+// so a half-wave's 32 lanes still read 32 distinct columns (bank = column).
+__device__ __forceinline__ uint32_t group_lin8_rot(const Lane8& L, const Chains& c, uint32_t e) {
+  const uint32_t R = 31u - e;
+  const uint32_t u = (L.rot - R) & 3u;
+  const bool r1 = (u & 1u) != 0, r2 = (u & 2u) != 0;
+  const uint32_t a01 = r1 ? c.v1 : c.v0, a12 = r1 ? c.v2 : c.v1, a23 = r1 ? c.v3 : c.v2, a30 = r1 ? c.v0 : c.v3;
+  const uint32_t X0 = r2 ? a23 : a01, X1 = r2 ? a30 : a12, X2 = r2 ? a01 : a23, X3 = r2 ? a12 : a30;
+  const uint32_t K2 = rot_nibble_key(L.col, u, e);
+  uint32_t v = xor3(nib_mul<0>(L.lds, X0, K2), nib_mul<1>(L.lds, X1, K2), nib_mul<2>(L.lds, X2, K2)) ^
+               nib_mul<3>(L.lds, X3, K2);
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
@@ -112,14 +137,24 @@ __device__ __forceinline__ uint4 fix_piece(const char* lds, uint4 x, int p) {
 }
 
 __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
-#if defined(UFC_TUNING) && defined(UFC_V8_ABL) && (UFC_V8_ABL & 1)  // ablation: no chain steps
-  c.v0 ^= x.x; c.v1 ^= x.y; c.v2 ^= x.z; c.v3 ^= x.w;
-  return;
-#endif
   c.v0 = chain_step(L.lds, c.v0, L.K, x.x);
   c.v1 = chain_step(L.lds, c.v1, L.K, x.y);
   c.v2 = chain_step(L.lds, c.v2, L.K, x.z);
   c.v3 = chain_step(L.lds, c.v3, L.K, x.w);
+}
+
+// One line of a frame whose stream may end inside it: lim = bytes of the lane's 16 before the end of
+// the CRC'd data.  Words before the frame's end (the data's and the trailer's) step their slots,
+// the trailer's bytes and those past the data as zeros; words past the frame's end do not step.
+__device__ __forceinline__ void chain4_masked(const Lane8& L, Chains& c, uint4 x, int lim) {
+  const uint32_t n0 = chain_step(L.lds, c.v0, L.K, x.x & data_mask(lim));
+  const uint32_t n1 = chain_step(L.lds, c.v1, L.K, x.y & data_mask(lim - 4));
+  const uint32_t n2 = chain_step(L.lds, c.v2, L.K, x.z & data_mask(lim - 8));
+  const uint32_t n3 = chain_step(L.lds, c.v3, L.K, x.w & data_mask(lim - 12));
+  c.v0 = lim > -4 ? n0 : c.v0;
+  c.v1 = lim > 0 ? n1 : c.v1;
+  c.v2 = lim > 4 ? n2 : c.v2;
+  c.v3 = lim > 8 ? n3 : c.v3;
 }
 
 // One 256-byte block j of a frame (pieces x0 at 16 col, x1 at 128 + 16 col, window-aligned):
@@ -165,48 +200,38 @@ __device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, u
 }
 
 struct Set8Meta {
-  uint32_t Jset;  // max J of the set's frames
+  uint32_t Pmax;  // most lines of the set's frames
+  uint32_t plim;  // lines 0 .. plim-1 hold CRC'd data only, in every frame of the set
   bool slow;      // byte path
-  bool mixed;     // block counts differ
-  bool g1;        // a frame's G straddles into block 1 (pad > 256)
 };
 
-template <int J>
-struct Buf8 {
-  uint4 x[2 * J];
+// A set's loads: slot 0 = line 0, slot 1 = the frame's last line, slot k >= 2 = line k - 1; tr =
+// the trailer (4 bytes at zo).
+struct Buf13 {
+  uint4 x[kV8Pieces];
+  uint32_t tr = 0;
 };
 
 }  // namespace
 
-// WAVES waves per workgroup (one workgroup per CU); DEPTH sets per wave in the ring (the set
-// computed plus DEPTH - 1 in flight).  p.offsets = the run-sorted records, p.offsets_csr = the
-// CSR offsets (nullptr for pairs: p.frame_len = the buffer length, relative offsets < 2^31).
-// SORTW: runs are ordered by block count within aligned windows of SORTW frames (64: the whole run;
-// 8: no reordering across sets, i.e. each set is 8 consecutive frames).
-// GEOR (with INSORT): each run's geometry is computed once per frame, in the frame's own lane,
-// before the sort (one frame per lane instead of once per set in each of a group's 8 lanes), and
-// the per-set facts (max block count, mixed counts, byte path, G in block 1) once per run with
-// half-row DPP reductions and ballots; a set then takes its two words per group with ds_bpermute
-// and its set-level bits with one readfirstlane.  Frames the fast path cannot take sort together
-// (key 7), so they spoil fewer sets.
-template <bool SEAL, bool PAIRS, int WAVES, int DEPTH, bool INSORT, int SORTW = 64, int AUX = kV8Aux, bool GEOR = false>
-__global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
-  static_assert(SORTW == 8 || SORTW == 16 || SORTW == 32 || SORTW == 64, "sort window");
-  static_assert(!GEOR || INSORT, "per-run geometry needs the in-kernel sort");
-  constexpr int JM = kV8Blocks;
+// One workgroup of kV8Waves waves per CU, 2 sets per wave in the ring (the set computed plus one in
+// flight).  p.offsets = the CSR offsets (n + 1) or, with PAIRS, the (start, end) pairs (p.frame_len =
+// the buffer length).  Each run of 64 frames is ordered by block count in the wave that takes it,
+// after each frame's fast-path geometry has been computed in the frame's own lane; the per-set
+// facts (max block count, mixed counts, byte path, G in block 1) come once per run from half-row
+// DPP reductions and ballots, and a set takes its two words per group with ds_bpermute and its
+// set-level bits with one readfirstlane.  Frames the fast path cannot take sort together (key 7),
+// so they spoil fewer sets.
+constexpr int kV8Waves = 12;
+template <bool SEAL, bool PAIRS>
+__global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
+  constexpr int WAVES = kV8Waves;
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
-#ifdef UFC_TUNING
-  const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
-#endif
   Lane8 L;
   init_lane8(L, lds, p.G);
   const uint64_t nfr = p.nframes;
   const uint32_t nruns = (uint32_t)((nfr + kRunFrames - 1) / kRunFrames);
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#ifdef UFC_TUNING
-  const uint32_t w = blockIdx.x * WAVES + wid;
-  uint32_t nk = 0;  // sets this wave computed (timeline dumps)
-#endif
   // Schedule: the workgroup owns a contiguous range of runs [WR0, WR1) (8 sets per run of 64
   // frames); wave i takes run WR0 + i first, then claims the next runs one at a time from a
   // counter in LDS (ds_add_rtn: lgkmcnt, not the vmcnt queue of the loads).  With a static run
@@ -220,42 +245,46 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   uint32_t run = WR0 + wid < WR1 ? WR0 + wid : kNoSet, pos = 0;
   bool exhausted = run == kNoSet;
 
-  // ---- INSORT: each run is ordered by block count inside the wave that takes it (replaces the
-  // sort_runs pre-pass and its 16-byte records).  Lane i reads frame i's offsets and the lanes'
-  // keys are ranked with ballots, as in sort_runs; the run's records then sit in lane = sorted
-  // position (SR, pushed with ds_permute) and a set's group takes its record with ds_bpermute.
-  // The next run is claimed, and its offsets loaded, one run ahead (raw_a / raw_b).
-  const uint64_t* offs = p.offsets;  // INSORT: CSR offsets (n + 1) or (start, end) pairs
+  // ---- Each run is ordered by block count inside the wave that takes it: lane i reads frame i's
+  // offsets, the lanes' keys are ranked with ballots, the run's per-frame words then sit in lane =
+  // sorted position (SR, pushed with ds_permute) and a set's group takes them with ds_bpermute.  The
+  // next run is claimed, and its offsets loaded, one run ahead (raw_a / raw_b).
+  const uint64_t* offs = p.offsets;
+  // A sorted run: lane = sorted position.  Fast path: a_lo = geometry | set facts, a_hi = window start,
+  // sb = the run base (wave-uniform).  Raw (the byte path): a_lo, a_hi = frame start, len, info = index
+  // | dead.
   struct SRec {
     uint32_t a_lo, a_hi, len, info;
+    uint64_t sb;
   };
-  SRec SR{0u, 0u, 0u, 0x80000000u};
+  SRec SR{0u, 0u, 0u, 0x80000000u, 0u};
   auto raw_load = [&](uint32_t r, uint64_t& a, uint64_t& b) {
     const uint64_t f = (uint64_t)(r == kNoSet ? 0u : r) * kRunFrames + L.lane;
     const uint64_t fi = f < nfr ? f : 0u;
     a = *as_global<g_u64>(offs + (PAIRS ? 2 * fi : fi));
     b = *as_global<g_u64>(offs + (PAIRS ? 2 * fi + 1 : fi + 1));
   };
-  const uint64_t buf_end = PAIRS ? p.frame_len : *as_global<g_u64>(p.offsets_csr + nfr);
   const bool flat = PAIRS && p.frame_len < (1ull << 31) - (1ull << 20);
-  // GEOR: the fast-path geometry of this lane's frame (unsorted), relative to the run's base sb
-  // (the run's first frame, or the buffer itself for flat pairs, minus the bias; wave-uniform).
+  // The fast-path geometry of this lane's frame (unsorted), relative to the run's base sb (the run's
+  // first frame, or the buffer itself for flat pairs, minus the bias; wave-uniform).  The window runs
+  // from the 128-byte line holding G's first byte (4 bytes before the frame) to the line holding the
+  // frame's last byte: every load is one whole line, and the lines a frame shares with its
+  // neighbours are its first and its last.  (A window may end past the buffer, inside the buffer's
+  // last line: that line's page holds the buffer's last byte.)
   struct FGeo {
     uint32_t geo, wrel;
     bool bad;
   };
   auto frame_geo = [&](uint64_t a, uint64_t len64, bool live, uint64_t sb) -> FGeo {
-    const uint32_t len = (uint32_t)min(len64, (uint64_t)0x40000000u);  // (longer: J > 6, the byte path)
-    const uint32_t t = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a + len)) & 3u;  // end up to 4 B
-    const uint32_t J = (len + t + 4u + 255u) >> 8;
-    const uint32_t pad = (J * 256u - len - t) & 511u;
+    const uint32_t len = (uint32_t)min(len64, (uint64_t)0x40000000u);  // (longer: past 13 lines, the byte path)
+    const uint32_t r = ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - 4u) & 127u;
+    const uint32_t zo = len + r;  // the trailer's first byte: (a + len - 4) - (a - 4 - r)
+    const uint32_t P = (zo + 131u) >> 7;
     const uint64_t rel64 = a - sb;
     FGeo g;
-    g.wrel = (uint32_t)rel64 - pad;  // window start (4-byte aligned)
-    g.bad = !live || len < 4u || J > (uint32_t)JM || a < (uint64_t)pad || a + len + 3 > buf_end ||
-            rel64 >= (uint64_t)kV8Limit || rel64 < 512u;
-    g.geo = pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | (L.lane << 16) |
-            ((live ? 0u : 1u) << 22) | ((g.bad ? 1u : 0u) << 23);
+    g.wrel = (uint32_t)rel64 - 4u - r;  // window start (128-byte aligned in memory)
+    g.bad = !live || len < 4u || P > (uint32_t)kV8Pieces || a < 4u + r || rel64 >= (uint64_t)kV8Limit || rel64 < 512u;
+    g.geo = r | (min(len, 2047u) << 7) | (L.lane << 18);
     return g;
   };
   auto run_base = [&](uint64_t a) -> uint64_t {
@@ -264,76 +293,67 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
                                      ~3ull);
     return b0 - kV8Bias;
   };
-  // RAW: permute the raw record (a, len, lane | dead) even in GEOR mode (the byte path's re-sort:
-  // the same keys, so the same permutation).
+  // Each run's frames ranked by key = pieces P (1..13), 14 = byte path, 15 = past the batch end.
+  // RAW: permute the raw record (a, len, lane | dead) instead of the geometry (the byte path's
+  // re-sort: the same keys, so the same permutation).
   auto sort_run = [&](uint32_t r, uint64_t a, uint64_t b, SRec& out, bool raw = false) {
     const uint64_t f = (uint64_t)r * kRunFrames + L.lane;
     const bool live = r != kNoSet && f < nfr;
     const uint64_t len = (live && b >= a) ? b - a : 0u;
-    const uint64_t n4 = len >= 4 ? len - 4 : len;
-    const uint64_t J = (n4 + 8 + 255) >> 8;
-    uint32_t key = !live ? 8u : ((len >= 4 && len < 0x40000000ull && J <= (uint64_t)JM) ? (uint32_t)J : 7u);
-    FGeo fg{0u, 0u, false};
-    uint64_t sb = 0;
-    if constexpr (GEOR) {
-      sb = run_base(a);
-      fg = frame_geo(a, len, live, sb);
-      key = !live ? 8u : (fg.bad ? 7u : (uint32_t)J);
-    }
-    if constexpr (SORTW == 8) {  // sets of consecutive frames: no reordering
-      out.a_lo = (uint32_t)a;
-      out.a_hi = (uint32_t)(a >> 32);
-      out.len = (uint32_t)min(len, (uint64_t)0xFFFFFFFFu);
-      out.info = L.lane | (live ? 0u : 0x80000000u);
-      return;
-    }
-    const uint64_t qmask = SORTW == 64 ? ~0ull : (((1ull << SORTW) - 1ull) << (L.lane & ~(uint32_t)(SORTW - 1)));
+    const uint64_t sb = run_base(a);
+    const FGeo fg = frame_geo(a, len, live, sb);
+    const uint32_t key = !live ? 15u : (fg.bad ? 14u : w_P(fg.geo));  // (a set with a dead frame: byte path)
     uint32_t below = 0, rank_in = 0;
 #pragma unroll
-    for (uint32_t k = 1; k <= 8; k++) {
-      const uint64_t m = __builtin_amdgcn_ballot_w64(key == k) & qmask;
+    for (uint32_t k = 1; k <= 15; k++) {
+      const uint64_t m = __builtin_amdgcn_ballot_w64(key == k);
       below += (k < key) ? (uint32_t)__builtin_popcountll(m) : 0u;
       const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       rank_in = (k == key) ? rk : rank_in;
     }
-    const int dst = (int)(((L.lane & ~(uint32_t)(SORTW - 1)) + below + rank_in) * 4u);
-    if constexpr (GEOR) {
-      if (!raw) {
-        // lane = sorted position: per-set facts over each 8-lane half-row, packed into geo bits 24..29
-        uint32_t geo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.geo);
-        out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.wrel);
-        out.len = (uint32_t)sb;
-        out.info = (uint32_t)(sb >> 32);
-        const uint32_t Jk = (geo >> 9) & 7u;
-        uint32_t jx = Jk, jn = Jk;
-        jx = max(jx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jx, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-        jn = min(jn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jn, 0xB1, 0xF, 0xF, false));
-        jx = max(jx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jx, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-        jn = min(jn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jn, 0x4E, 0xF, 0xF, false));
-        jx = max(jx, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jx, 0x141, 0xF, 0xF, false));  // row_half_mirror
-        jn = min(jn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)jn, 0x141, 0xF, 0xF, false));
-        const uint64_t mbad = __builtin_amdgcn_ballot_w64(((geo >> 23) & 1u) != 0);
-        const uint64_t mg1 = __builtin_amdgcn_ballot_w64((geo & 511u) > 256u);
-        const uint32_t s8 = L.lane & ~7u;
-        const uint32_t slow = ((mbad >> s8) & 0xFFu) != 0 ? 1u : 0u, g1 = ((mg1 >> s8) & 0xFFu) != 0 ? 1u : 0u;
-        out.a_lo = geo | (min(jx, (uint32_t)JM) << 24) | ((jx != jn ? 1u : 0u) << 27) | (slow << 28) | (g1 << 29);
-        return;
-      }
+    const int dst = (int)((below + rank_in) * 4u);
+    if (!raw) {
+      // lane = sorted position: per-set facts over each 8-lane half-row, into geo bits 24..31
+      const uint32_t geo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.geo);
+      const uint32_t bad = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(key >= 14u ? 1u : 0u));
+      out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.wrel);
+      out.sb = sb;
+      uint32_t px = w_P(geo), zn = w_zo(geo) >> 7;
+      px = max(px, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)px, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+      zn = min(zn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)zn, 0xB1, 0xF, 0xF, false));
+      px = max(px, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)px, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+      zn = min(zn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)zn, 0x4E, 0xF, 0xF, false));
+      px = max(px, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)px, 0x141, 0xF, 0xF, false));  // row_half_mirror
+      zn = min(zn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)zn, 0x141, 0xF, 0xF, false));
+      const uint64_t mbad = __builtin_amdgcn_ballot_w64(bad != 0u);
+      const bool slow = ((mbad >> (L.lane & ~7u)) & 0xFFu) != 0;
+      out.a_lo = (geo & 0xFFFFFFu) | ((slow ? 0u : min(px, 15u)) << 24) | (min(zn, 15u) << 28);
+      return;
     }
     out.a_lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)a);
     out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(a >> 32));
     out.len = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)min(len, (uint64_t)0xFFFFFFFFu));
     out.info = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(L.lane | (live ? 0u : 0x80000000u)));
   };
-  auto take_rec = [&](const SRec& sr, uint32_t q, bool raw = false) -> uint4 {
+  // The raw words of this group's frame of set q (the same in the group's 8 lanes): start lo, hi,
+  // length, index | dead.
+  auto take_raw = [&](const SRec& sr, uint32_t q) -> uint4 {
     const int src = (int)(((q & 7u) * 8u + L.grp) * 4u);
-    if (GEOR && !raw)
-      return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_lo),
-                        (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_hi), sr.len, sr.info);
     return make_uint4((uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_lo),
                       (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_hi),
                       (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.len),
                       (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.info));
+  };
+  // Set q's words: geometry | set facts and window start (the same in the group's 8 lanes), the run
+  // base (wave-uniform: scalar registers).
+  struct Rec {
+    uint32_t geo, wrel;
+    uint64_t sb;
+  };
+  auto take_rec = [&](const SRec& sr, uint32_t q) -> Rec {
+    const int src = (int)(((q & 7u) * 8u + L.grp) * 4u);
+    return Rec{(uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_lo),
+               (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)sr.a_hi), sr.sb};
   };
   uint32_t run_nxt = kNoSet;
   uint64_t raw_a = 0, raw_b = 0;
@@ -346,19 +366,14 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       if (WR0 + v < WR1) run_nxt = WR0 + v;
       else exhausted = true;
     }
-    if constexpr (INSORT) raw_load(run_nxt, raw_a, raw_b);
+    raw_load(run_nxt, raw_a, raw_b);
   };
   auto next_q = [&]() -> uint32_t {
     if (pos == 8u) {
       pos = 0;
-      if constexpr (INSORT) {
-        run = run_nxt;
-        sort_run(run, raw_a, raw_b, SR);
-        claim_next();
-      } else {
-        claim_next();
-        run = run_nxt;
-      }
+      run = run_nxt;
+      sort_run(run, raw_a, raw_b, SR);
+      claim_next();
     }
     const uint32_t q = run == kNoSet ? kNoSet : run * 8u + pos;
     pos++;
@@ -366,85 +381,59 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   };
   // the wave's first run: offsets first (loads in flight while the tables' loads are issued)
   uint64_t a0 = 0, b0 = 0;
-  if constexpr (INSORT) raw_load(run, a0, b0);
+  raw_load(run, a0, b0);
   const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
-  if constexpr (INSORT) sort_run(run, a0, b0, SR);
-  const uint4* rec = (const uint4*)p.offsets;
+  sort_run(run, a0, b0, SR);
 
-  // This group's record of set q (the same 16 bytes in the group's 8 lanes).
-  auto load_rec = [&](uint32_t q) -> uint4 {
-    if constexpr (INSORT) return take_rec(SR, q);
-    const uint32_t qc = q == kNoSet ? 0u : q;  // (no set: reads set 0)
-    const u32x4 r = *as_global<g_u32x4>((const uint32_t*)(rec + (uint64_t)qc * 8 + L.grp));
-    return make_uint4(r.x, r.y, r.z, r.w);
-  };
-  // Geometry of the wave's set k from its record: packed per-lane geometry, block-0 piece-0
-  // offset, meta, and the set's base (buffer offset of its loads' resource, minus a bias): its
-  // group-0 frame's start (CSR: the fast frames of a run lie within 64 x 1.5 KB of each other),
-  // or the buffer itself for pairs over less than 2 GB (pairs may come in any order).
-  auto geometry = [&](uint32_t q, uint4 r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
-    if constexpr (GEOR) {  // r = (geo | set bits, window start, run base lo, hi) from the run's sort
-      sb = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.z) |
-           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.w) << 32);
-      const uint32_t gu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.x);
-      m.Jset = (gu >> 24) & 7u;
-      m.mixed = ((gu >> 27) & 1u) != 0;
-      m.slow = ((gu >> 28) & 1u) != 0;
-      m.g1 = ((gu >> 29) & 1u) != 0;
-      const bool live = q != kNoSet && !m.slow;
-      voff0 = live ? r.y + 16u * L.col : kV8Oob;
-      return r.x & 0x7FFFFFu;
-    }
-    const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
-    const uint32_t len = min(r.z, 0x40000000u);  // (longer: J > 6, the byte path)
-    const bool dead = (r.w >> 31) != 0;
-    const uint32_t t = (0u - ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a + len)) & 3u;  // end up to 4 B
-    const uint32_t J = (len + t + 4u + 255u) >> 8;
-    const uint32_t pad = (J * 256u - len - t) & 511u;
-    sb = flat ? 0u : (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.x) |
-                       ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r.y) << 32)) & ~3ull);
-    sb -= kV8Bias;
-    const uint64_t rel64 = a - sb;
-    const uint32_t wrel = (uint32_t)rel64 - pad;  // window start (4-byte aligned)
-    const bool bad = dead || len < 4u || J > (uint32_t)JM || a < (uint64_t)pad || a + len + 3 > buf_end ||
-                     rel64 >= (uint64_t)kV8Limit || rel64 < 512u;
-    m.slow = __builtin_amdgcn_ballot_w64(bad) != 0;
-    uint32_t jmax = 0, jmin = 7;
-#pragma unroll
-    for (int g = 0; g < 8; g++) {
-      const uint32_t jg = (uint32_t)__builtin_amdgcn_readlane((int)J, 8 * g);
-      jmax = max(jmax, jg);
-      jmin = min(jmin, jg);
-    }
-    m.Jset = min(jmax, (uint32_t)JM);
-    m.mixed = jmin != jmax;
-    m.g1 = __builtin_amdgcn_ballot_w64(pad > 256u) != 0;
+  auto load_rec = [&](uint32_t q) -> Rec { return take_rec(SR, q); };
+  // Geometry of set q from its words: per-lane geometry, the lane's line-0 offset, the set facts, the
+  // run base (the buffer offset of the loads' resource, minus a bias: the run's first frame's start,
+  // or the buffer itself for flat pairs).
+  auto geometry = [&](uint32_t q, const Rec& r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
+    sb = r.sb;
+    const uint32_t gu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.geo);
+    m.Pmax = (gu >> 24) & 15u;
+    m.plim = gu >> 28;
+    m.slow = m.Pmax == 0u;
     const bool live = q != kNoSet && !m.slow;
-    voff0 = live ? wrel + 16u * L.col : kV8Oob;
-    return pad | (min(J, 7u) << 9) | ((len >= 5u ? 1u : 0u) << 12) | (t << 13) | ((r.w & 63u) << 16) |
-           ((dead ? 1u : 0u) << 22);
+    voff0 = live ? r.wrel + 16u * L.col : kV8Oob;
+    return r.geo;
   };
-  // The set's loads: block j's pieces at voff0 + 256 j (+ 128); pieces wholly before the frame
-  // and blocks past it are out of range.
-  auto load_set = [&](uint32_t voff0, uint32_t geo, uint64_t sb, Buf8<JM>& b) {
-    const uint32_t J = v8_J(geo), pad = v8_pad(geo);
+  // The set's loads (struct Buf13): slots 0 and 1, the lines the frame shares with its neighbours
+  // (which the sort puts in other sets), with default policy so that they stay in L2 for them; the
+  // lines in between, each read by this set alone, non-temporal; lanes wholly before G, lines past the
+  // frame's own and a frame's second slot when it has one line are out of range (zeros, no request).
+  // Then the trailer, one dword at zo.
+  // Issued in two parts (PART 0: slots 0 and 2 .. kV8Split - 1 and the trailer; PART 1: the rest), the
+  // second in the middle of the previous set's compute, once its first lines' registers are free.
+  auto load_set = [&](uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b, auto part) {
+    constexpr int PART = decltype(part)::value;
+    const uint32_t P = w_P(geo), front = w_r(geo) + 4u;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
-    // one select per block (the constant part of each offset goes into the instruction's offset
-    // field; an out-of-range base stays out of range with it).  Every block's load is issued, past
-    // the set's block count too: skipping them under a wave-uniform branch measured 2.29 against
-    // 1.52 ms (the compiler's wait counts no longer match, and it waits for everything).
+    if constexpr (PART == 0) {
+      const uint32_t vo = (16u * L.col + 16u <= front) ? kV8Oob : voff0;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8AuxShared);
+      b.x[0] = make_uint4(v.x, v.y, v.z, v.w);
+    }
 #pragma unroll
-    for (int j = 0; j < JM; j++) {
-      const uint32_t base = ((uint32_t)j < J) ? voff0 : kV8Oob;
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        uint32_t vo = base;
-        if (j == 0) vo = (128u * h + 16u * L.col + 16u <= pad) ? kV8Oob : vo;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 256u * j + 128u * h), 0, AUX);
-        b.x[2 * j + h] = make_uint4(v.x, v.y, v.z, v.w);
+    for (int k = PART == 0 ? 2 : kV8Split; k < (PART == 0 ? kV8Split : kV8Pieces); k++) {  // line k - 1
+      const uint32_t vo = (uint32_t)k + 1u <= P ? voff0 : kV8Oob;  // (an out-of-range base stays out of range)
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)(k - 1)), 0, kV8AuxInterior);
+      b.x[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    if constexpr (PART == 0) {
+      if constexpr (!SEAL) {
+        const uint32_t vt = voff0 == kV8Oob ? kV8Oob : voff0 - 16u * L.col + w_zo(geo);
+        b.tr = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vt, 0, kV8AuxShared);
       }
+    } else {
+      const uint32_t vo = P >= 2u ? voff0 + 128u * (P - 1u) : kV8Oob;
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8AuxShared);
+      b.x[1] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
+  using Part0 = std::integral_constant<int, 0>;
+  using Part1 = std::integral_constant<int, 1>;
 
   // ---- results of the current run: lane (g, col = t) <- set t's frame g; qv = orig | valid << 31
   uint32_t acc_crc = 0, acc_qv = 0;
@@ -459,62 +448,78 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_qv >> 31);
     }
   };
-  // A^-t of every group's lin (t from the geometry; the 32-slot image's columns 40 + 3 (g & 3) +
-  // t - 1 hold the nibble tables, one copy per group of a half-wave: no bank conflicts).
-  auto unshift = [&](uint32_t lin, uint32_t geo) -> uint32_t {
-    const uint32_t t = v8_t(geo);
+  // A^-t of every group's lin (the 32-slot image's columns 40 + 3 (g & 3) + t - 1 hold the nibble
+  // tables, one copy per group of a half-wave: no bank conflicts).
+  auto unshift = [&](uint32_t lin, uint32_t t) -> uint32_t {
     if (__builtin_amdgcn_ballot_w64(t != 0) == 0) return lin;
     const uint32_t col = 40u + 3u * (L.grp & 3u) + (t ? t - 1u : 0u);
     const uint32_t r = nib_mul<0>(L.lds, lin, col * 4u);
     return t ? r : lin;
   };
-  // The result of a set (crc in every lane of a group; trailer word in its lane 7).
-  auto finish = [&](uint32_t q, uint32_t geo, const Chains& c, uint32_t voff0, uint64_t sb) {
-#if defined(UFC_TUNING) && defined(UFC_V8_ABL) && (UFC_V8_ABL & 2)  // ablation: no slot combine
-    const uint32_t crc = ~(c.v0 ^ c.v1 ^ c.v2 ^ c.v3 ^ geo);
-#else
-    const uint32_t crc = ~unshift(group_lin8(L, c), geo);
-#endif
-    const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
-    const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
-    if (SEAL && L.col == 7u && !((geo >> 22) & 1u)) {  // BE32 trailer: one dword store from lane 7
-      // (4-byte aligned when t = 0; otherwise an unaligned dword store, which gfx950's unaligned access
-      // mode splits in the memory pipeline: one store instruction per frame instead of four byte stores)
-      // (non-temporal trailer stores measured slower: 1.912 against 1.874 ms, DESIGN.md section 5.3)
-      uint32_t* const ta = (uint32_t*)((uint8_t*)p.wbytes + sb + (voff0 - 16u * L.col + 256u * v8_J(geo) - v8_t(geo) - 4u));
-      st_u32_hidden(ta, __builtin_bswap32(crc));
-    }
-    record(q & 7u, crc, v8_orig(geo) | (ok << 31) | (((geo >> 22) & 1u) << 30));
-    if ((q & 7u) == 7u) store_run(q >> 3);
-  };
 
-  // Fast set: Jset blocks (uniform), the loaded pieces as they are.
-  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf8<JM>& b, uint32_t voff0, uint64_t sb) {
-    const uint32_t J = v8_J(geo), pad = v8_pad(geo), t = v8_t(geo);
+  // Fast set.  The stream of a frame is its window with the bytes before G zeroed, G, the data, the
+  // trailer as zeros, up to the end of the word holding the frame's last byte (e: that word's slot,
+  // t = 0..3 bytes past the frame in it): lin = A^t (register after the data), undone at the finish.
+  // Line order: slot 0 (line 0), slots 2.. (lines 1 .. P-2), slot 1 (line P-1); lines past a frame's
+  // own step nothing (masked), so every frame's slots see its lines in order.
+  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf13& b, uint32_t voff0, uint64_t sb, auto mid) {
+    const uint32_t zo = w_zo(geo), P = w_P(geo), front = w_r(geo) + 4u;
+    const int lim0 = (int)zo - (int)(16u * L.col);
     Chains c{0u, 0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int j = 0; j < JM; j++) {
-      if ((uint32_t)j < m.Jset) {
-        if (m.mixed)
-          block8<true>(L, (uint32_t)j, J, pad, t, m.g1, false, b.x[2 * j], b.x[2 * j + 1], c);
-        else
-          block8<false>(L, (uint32_t)j, J, pad, t, m.g1, (uint32_t)j + 1 == m.Jset, b.x[2 * j], b.x[2 * j + 1], c);
+    {  // line 0: zeros before G, G, the frame's first bytes
+      const uint4 x = fix_piece(L.lds, b.x[0], (int)front - (int)(16u * L.col));
+      if (m.plim >= 1u) {
+        c.v0 = x.x;
+        c.v1 = x.y;
+        c.v2 = x.z;
+        c.v3 = x.w;
+      } else {
+        c.v0 = x.x & data_mask(lim0);
+        c.v1 = x.y & data_mask(lim0 - 4);
+        c.v2 = x.z & data_mask(lim0 - 8);
+        c.v3 = x.w & data_mask(lim0 - 12);
       }
     }
-    finish(q, geo, c, voff0, sb);
+#pragma unroll
+    for (int j = 1; j < kV8Pieces - 1; j++) {  // line j from slot j + 1
+      if (j + 1 == kV8Split) {  // slots 2 .. kV8Split - 1 consumed: the next set's second part
+        __builtin_amdgcn_sched_barrier(0);
+        mid();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      uint4 x = b.x[j + 1];
+      if (j == 1) x.x = fix_word(x.x, 128 + (int)(16u * L.col) - (int)front, L.G);  // G's last bytes (r >= 125)
+      if ((uint32_t)j < m.plim)
+        chain4(L, c, x);
+      else if ((uint32_t)j + 1u < m.Pmax)
+        chain4_masked(L, c, x, (uint32_t)j + 1u < P ? lim0 - 128 * j : -4);
+    }
+    if (m.Pmax >= 2u) {  // the last line (a one-line frame: no step)
+      uint4 x = b.x[1];
+      if (P == 2u) x.x = fix_word(x.x, 128 + (int)(16u * L.col) - (int)front, L.G);
+      chain4_masked(L, c, x, P >= 2u ? lim0 - 128 * (int)(P - 1u) : -4);
+    }
+    const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
+    const uint32_t crc = ~unshift(group_lin8_rot(L, c, e), t);
+    const uint32_t ok = (!SEAL && w_len(geo) >= 5u && __builtin_bswap32(b.tr) == crc) ? 1u : 0u;
+    if (SEAL && L.col == 0u) {  // BE32 trailer: one (unaligned) dword store per frame
+      // (non-temporal trailer stores measured slower: 1.912 against 1.874 ms, DESIGN.md section 5.3)
+      uint32_t* const ta = (uint32_t*)((uint8_t*)p.wbytes + sb + (voff0 + zo));
+      st_u32_hidden(ta, __builtin_bswap32(crc));
+    }
+    record(q & 7u, crc, w_orig(geo) | (ok << 31));
+    if ((q & 7u) == 7u) store_run(q >> 3);
   };
 
   // Byte path of set q: any lengths, loads restricted to each frame; the same result handling.
   auto slow_set = [&](uint32_t q) {
     uint4 r;
-    if constexpr (INSORT) {  // (the run may have left SR: sort it again)
+    {  // (the run may have left SR: sort it again)
       uint64_t a, b;
       SRec T;
       raw_load(q >> 3, a, b);
       sort_run(q >> 3, a, b, T, true);
-      r = take_rec(T, q, true);
-    } else {
-      r = load_rec(q);
+      r = take_raw(T, q);
     }
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
     const bool dead = (r.w >> 31) != 0;
@@ -539,13 +544,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       }
       uint32_t x[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const int ob = o + 4 * i;  // frame offset of the word's first byte
-        const uint32_t lo = (uint32_t)min(max(-ob, 0), 4), hi = (uint32_t)min(max((int)d.len - ob, 0), 4);
-        const uint32_t mhi = hi >= 4u ? ~0u : ((1u << ((8u * hi) & 31u)) - 1u),  // (amounts kept in range)
-                       mlo = lo >= 4u ? 0u : (~0u << ((8u * lo) & 31u));
-        x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh) & mhi & mlo;
-      }
+      for (int i = 0; i < 4; i++)  // (o + 4 i: the frame offset of the word's first byte)
+        x[i] = __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh) & frame_word_mask(o + 4 * i, d.len);
       return make_uint4(x[0], x[1], x[2], x[3]);
     };
 #pragma unroll 1
@@ -556,10 +556,9 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       const uint4 x1 = piece(o0 + 128);
       block8<true>(L, j, (uint32_t)d.J, (uint32_t)d.pad, 0u, true, false, x0, x1, c);
     }
-    const uint32_t geo = ((d.len >= 5u ? 1u : 0u) << 12) | ((r.w & 63u) << 16) | ((dead ? 1u : 0u) << 22);
     const uint32_t crc = ~group_lin8(L, c);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((L.lane | 7u) * 4u), (int)c.tr);
-    const uint32_t ok = (((geo >> 12) & 1u) && __builtin_bswap32(tr) == crc) ? 1u : 0u;
+    const uint32_t ok = (d.len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     if (SEAL && L.col == 7u && !dead && d.len >= 4u) {
       g_u8w* wp = as_global<g_u8w>(p.wbytes + d.start + d.n);
       wp[0] = (uint8_t)(crc >> 24);
@@ -567,21 +566,21 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
       wp[2] = (uint8_t)(crc >> 8);
       wp[3] = (uint8_t)crc;
     }
-    record(q & 7u, crc, v8_orig(geo) | (ok << 31) | ((dead ? 1u : 0u) << 30));
+    record(q & 7u, crc, (r.w & 63u) | (ok << 31) | ((dead ? 1u : 0u) << 30));
     if ((q & 7u) == 7u) store_run(q >> 3);
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no visible load or store stays pending
   };
 
   // ---- ring: set S_k in slot k % DEPTH; records DEPTH sets ahead of their geometry ----
-  static_assert(DEPTH == 2 || DEPTH == 3, "ring depth");
-  Buf8<JM> B[DEPTH];
-  uint4 O[DEPTH];
+  constexpr int DEPTH = 2;
+  Buf13 B[DEPTH];
+  Rec O[DEPTH];
   uint32_t GE[DEPTH], VO[DEPTH], QO[DEPTH], QG[DEPTH];  // set of O[i] / of GE[i], B[i]
   uint64_t SB[DEPTH];
   Set8Meta M[DEPTH];
   // prologue: records of the wave's first 2 DEPTH - 1 sets, geometry + loads of the first
   // DEPTH - 1 (all in the wave's first run, which needs no claim: 2 DEPTH - 1 <= 8)
-  uint4 Rq[DEPTH];
+  Rec Rq[DEPTH];
   uint32_t Qq[DEPTH];
 #pragma unroll
   for (int i = 0; i < DEPTH; i++) {
@@ -592,7 +591,8 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   for (int i = 0; i < DEPTH - 1; i++) {
     QG[i] = Qq[i];
     GE[i] = geometry(QG[i], Rq[i], VO[i], M[i], SB[i]);
-    load_set(VO[i], GE[i], SB[i], B[i]);
+    load_set(VO[i], GE[i], SB[i], B[i], Part0{});
+    load_set(VO[i], GE[i], SB[i], B[i], Part1{});
     QO[i] = next_q();
     O[i] = load_rec(QO[i]);
   }
@@ -606,128 +606,64 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_varlen8_kernel(const Ker
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-#ifdef UFC_TUNING
-  const unsigned long long t_staged = __builtin_amdgcn_s_memrealtime();
-#endif
-  if constexpr (INSORT) claim_next();  // the second run (the counter is set now)
+  claim_next();  // the second run (the counter is set now)
 
   // One step: geometry + loads of set S + DEPTH - 1 (record loaded DEPTH steps ago), the record of
   // set S + 2 DEPTH - 1, then compute set S.
   auto step = [&](int cs, int fs) {
     QG[fs] = QO[fs];
     GE[fs] = geometry(QG[fs], O[fs], VO[fs], M[fs], SB[fs]);
-    load_set(VO[fs], GE[fs], SB[fs], B[fs]);
+    load_set(VO[fs], GE[fs], SB[fs], B[fs], Part0{});
     QO[fs] = next_q();
     O[fs] = load_rec(QO[fs]);
     __builtin_amdgcn_sched_barrier(0);
-    if (QG[cs] != kNoSet) {
-      if (!M[cs].slow)
-        compute(QG[cs], GE[cs], M[cs], B[cs], VO[cs], SB[cs]);
-      else
-        slow_set(QG[cs]);
-#ifdef UFC_TUNING
-      nk++;
-#endif
+    auto second = [&]() { load_set(VO[fs], GE[fs], SB[fs], B[fs], Part1{}); };
+    if (QG[cs] != kNoSet && !M[cs].slow) {
+      compute(QG[cs], GE[cs], M[cs], B[cs], VO[cs], SB[cs], second);
+    } else {
+      second();
+      if (QG[cs] != kNoSet) slow_set(QG[cs]);
     }
     __builtin_amdgcn_sched_barrier(0);
   };
   // (a wave's sets are valid up to its first kNoSet, so a round stops at the first dead set)
-  if constexpr (DEPTH == 3) {
-    while (QG[0] != kNoSet) {
-      step(0, 2);
-      step(1, 0);
-      step(2, 1);
-    }
-  } else {
-    while (QG[0] != kNoSet) {
-      step(0, 1);
-      step(1, 0);
-    }
+  while (QG[0] != kNoSet) {
+    step(0, 1);
+    step(1, 0);
   }
-#ifdef UFC_TUNING
-  if (p.dbg && L.lane == 0) {  // per-wave timeline (tools/wave_timeline.py)
-    const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
-    unsigned long long* d = p.dbg + 4 * w;
-    d[0] = t_start;
-    d[1] = t_staged;
-    d[2] = t_end;
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);  // HW_REG_XCC_ID[3:0]
-    d[3] = (unsigned long long)nk | ((unsigned long long)__smid() << 32) | ((unsigned long long)xcc << 56);
-  }
-#endif
 }
 
-#define UFC_V8_INST(SEAL, PAIRS, IS) \
-  template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, 12, 2, IS>(const KernelParams);
-#define UFC_V8_INSTW(SEAL, SW) \
-  template __global__ void frame_crc_varlen8_kernel<SEAL, false, 12, 2, true, SW>(const KernelParams);
-#define UFC_V8_INSTA(SW) \
-  template __global__ void frame_crc_varlen8_kernel<false, false, 12, 2, true, SW, 2>(const KernelParams);
-#define UFC_V8_INSTG(SEAL, PAIRS) \
-  template __global__ void frame_crc_varlen8_kernel<SEAL, PAIRS, 12, 2, true, 64, kV8Aux, true>(const KernelParams);
 // Product: 12 waves, 2 sets per wave in the ring (three waves per SIMD; config 3 1.69 ms kernel
-// against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill), runs sorted
-// in the kernel with per-run geometry (GEOR: 1.480 against 1.506 ms, config 3, in-process A/B,
-// identical results).  Per-set geometry and the pre-sorted variant (records from sort_runs) are
-// kept for A/B in tuning builds.
-UFC_V8_INSTG(false, false) UFC_V8_INSTG(true, false) UFC_V8_INSTG(false, true) UFC_V8_INSTG(true, true)
-#ifdef UFC_TUNING
-UFC_V8_INST(false, false, true) UFC_V8_INST(true, false, true) UFC_V8_INST(false, true, true) UFC_V8_INST(true, true, true)
-UFC_V8_INST(false, false, false) UFC_V8_INST(true, false, false) UFC_V8_INST(false, true, false) UFC_V8_INST(true, true, false)
-UFC_V8_INSTW(false, 8) UFC_V8_INSTW(false, 16) UFC_V8_INSTW(false, 32) UFC_V8_INSTW(true, 8) UFC_V8_INSTW(true, 16)
-UFC_V8_INSTW(true, 32) UFC_V8_INSTA(8) UFC_V8_INSTA(16) UFC_V8_INSTA(32) UFC_V8_INSTA(64)
-#endif
-#undef UFC_V8_INST
-#undef UFC_V8_INSTW
-#undef UFC_V8_INSTA
-#undef UFC_V8_INSTG
+// against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill), runs sorted in
+// the kernel with per-run geometry (1.480 against 1.506 ms with per-set geometry, config 3,
+// in-process A/B, identical results; profiles/EXPERIMENTS.md).
+template __global__ void frame_crc_varlen8_kernel<false, false>(const KernelParams);
+template __global__ void frame_crc_varlen8_kernel<true, false>(const KernelParams);
+template __global__ void frame_crc_varlen8_kernel<false, true>(const KernelParams);
+template __global__ void frame_crc_varlen8_kernel<true, true>(const KernelParams);
 
-const void* varlen8_kernel_symbol(bool seal, bool pairs, bool insort, int sortw, int aux, bool geor) {
-  if (geor) {
-    if (!insort || sortw != 64 || aux != kV8Aux) return nullptr;
-    if (pairs)
-      return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true, 64, kV8Aux, true>
-                  : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, true, 64, kV8Aux, true>;
-    return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 64, kV8Aux, true>
-                : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, kV8Aux, true>;
-  }
-#ifdef UFC_TUNING
-  if (insort && !pairs && !seal && aux == 2) {  // A/B: non-temporal loads (CSR validate)
-    switch (sortw) {
-      case 8: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 8, 2>;
-      case 16: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 16, 2>;
-      case 32: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 32, 2>;
-      case 64: return (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 64, 2>;
-      default: return nullptr;
-    }
-  }
-  if (aux != kV8Aux) return nullptr;
-  if (insort && !pairs && sortw != 64) {  // A/B: narrower sort windows (CSR)
-    switch (sortw) {
-      case 8: return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 8>
-                          : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 8>;
-      case 16: return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 16>
-                           : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 16>;
-      case 32: return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true, 32>
-                           : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true, 32>;
-      default: return nullptr;
-    }
-  }
-  if (insort) {  // per-set geometry (the round-3 product)
-    if (pairs)
-      return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, true>
-                  : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, true>;
-    return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, true>
-                : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, true>;
-  }
+const void* varlen8_kernel_symbol(bool seal, bool pairs) {
   if (pairs)
-    return seal ? (const void*)frame_crc_varlen8_kernel<true, true, 12, 2, false>
-                : (const void*)frame_crc_varlen8_kernel<false, true, 12, 2, false>;
-  return seal ? (const void*)frame_crc_varlen8_kernel<true, false, 12, 2, false>
-              : (const void*)frame_crc_varlen8_kernel<false, false, 12, 2, false>;
-#else
-  return nullptr;
-#endif
+    return seal ? (const void*)frame_crc_varlen8_kernel<true, true> : (const void*)frame_crc_varlen8_kernel<false, true>;
+  return seal ? (const void*)frame_crc_varlen8_kernel<true, false> : (const void*)frame_crc_varlen8_kernel<false, false>;
+}
+int varlen8_waves() { return kV8Waves; }
+
+__global__ __launch_bounds__(256) void slots_to_pairs_kernel(const uint32_t* lens, uint64_t stride, uint64_t n,
+                                                              uint64_t* pairs) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    const uint64_t a = i * stride;
+    pairs[2 * i] = a;
+    pairs[2 * i + 1] = a + lens[i];
+  }
+}
+
+int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(slots_to_pairs_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     d_lens, stride, n, d_pairs);
+  return (int)hipGetLastError();
 }
 
 }  // namespace ufc_dev

@@ -89,9 +89,7 @@ struct DevBytesHead {
     }
     return r;
   }
-  __device__ uint32_t held_byte(uint32_t i) const {  // (shift amounts always in range)
-    return (uint32_t)((i < 8 ? w0 : w1) >> (8 * (i & 7u))) & 0xFFu;
-  }
+  __device__ uint32_t held_byte(uint32_t i) const { return head_byte(w0, w1, i); }
   __device__ uint32_t operator()(uint32_t i) const {
     if (i < held) return held_byte(i);
     return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
@@ -528,9 +526,6 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   hipError_t e = hipMemsetAsync(cursor, 0, 8, stream);
   if (e != hipSuccess) return e;
   bool pool = true;  // pooled header slots (more walking frames per CU); UFC_WALK_POOL=0 (tuning): fixed slots
-#ifdef UFC_TUNING
-  if (const char* w = std::getenv("UFC_WALK_POOL")) pool = std::atoi(w) != 0;
-#endif
   if (pool)
     parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
                                                                            counts, modes, pos_seg, cursor, bases,
@@ -549,22 +544,6 @@ hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, 
   // without; the exact-offset load 0.453 against 0.458 for the aligned pair; non-temporal loads 0.447
   // against 0.453; non-temporal stores 0.426 against 0.430 on a faster box: DESIGN.md section 5.5).
   auto emit = parse_emit_kernel<1, 2, kEmitAux, true>;
-#ifdef UFC_TUNING
-  {  // UFC_EMIT_U=1|2|4 items per thread per round, UFC_EMIT_X4=0: five dword loads per header,
-     // 2: one unaligned 16-byte load at the header
-    const char* wu = std::getenv("UFC_EMIT_U");
-    const char* wx = std::getenv("UFC_EMIT_X4");
-    const int eu = wu ? std::atoi(wu) : 1;
-    const int x4 = wx ? std::atoi(wx) : 2;
-    if (eu == 2) emit = x4 == 2 ? parse_emit_kernel<2, 2> : x4 ? parse_emit_kernel<2, 1> : parse_emit_kernel<2, 0>;
-    else if (eu == 4) emit = x4 == 2 ? parse_emit_kernel<4, 2> : x4 ? parse_emit_kernel<4, 1> : parse_emit_kernel<4, 0>;
-    else emit = x4 == 2 ? parse_emit_kernel<1, 2, kEmitAux, true> : x4 ? parse_emit_kernel<1, 1> : parse_emit_kernel<1, 0>;
-    if (const char* w = std::getenv("UFC_EMIT_AUX"))  // cache policy of the header loads (0: default)
-      emit = std::atoi(w) == 0 ? parse_emit_kernel<1, 2, 0, true> : parse_emit_kernel<1, 2, kEmitAux, true>;
-    if (const char* w = std::getenv("UFC_EMIT_NTSTORE"))  // 0: the item records' stores default policy
-      if (std::atoi(w) == 0) emit = parse_emit_kernel<1, 2, kEmitAux, false>;
-  }
-#endif
   emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
                                                                     wg_firsts, modes, pos_seg, bases, a.items, a.items_cap,
                                                                     a.items_used);

@@ -9,6 +9,12 @@
 
 namespace ufc_dev {
 
+// Byte i (0..15) of a frame's first 16 bytes held as two little-endian words (the parse walk's head,
+// frame_parse.hip DevBytesHead): shift amounts always in range (host and device; tests/c/ubsan_helpers.hip).
+__host__ __device__ __forceinline__ uint32_t head_byte(uint64_t w0, uint64_t w1, uint32_t i) {
+  return (uint32_t)(((i & 15u) < 8 ? w0 : w1) >> (8 * (i & 7u))) & 0xFFu;
+}
+
 struct ParseArgs {
   const uint8_t* bytes;
   const uint64_t* offsets;

@@ -63,7 +63,7 @@ constexpr uint32_t kCtrSlots = 64;
 
 namespace {
 
-enum ScratchKind { kScratchParse = 0, kScratchSortRec = 1, kScratchAsyncSlots = 2, kScratchSealCrc = 3 };
+enum ScratchKind { kScratchParse = 0, kScratchAsyncSlots = 2, kScratchSealCrc = 3 };
 
 // The (kind, stream) scratch buffer of at least `need` bytes.  Growing waits for the work already
 // queued on that stream (the only user of the old buffer) before freeing it.
@@ -150,29 +150,8 @@ int lean_fixed_blocks(const ufc_ctx* ctx, uint64_t frame_len, uint64_t stride, u
 // front_ok: the bytes before the batch's first frame are readable (a later part of a larger batch).
 int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream,
                       bool front_ok = false) {
-  int depth = ufc_dev::kLeanDepthDefault, abl = 0, waves = ufc_dev::kLeanWavesDefault;
-  int sched = ufc_dev::kLeanSchedDefault;
-  if (ctx->opt[UFC_OPT_FIXED_KERNEL] == UFC_FIXED_CLAIM16) {  // A/B: the round-1 default
-    depth = 3;
-    sched = ufc_dev::kSchedClaim;
-    waves = 16;
-  }
-#ifdef UFC_TUNING
-  // A/B knobs of the validate path (tuning builds): pipeline depth, schedule, ablations.
-  if (!seal) {
-    if (const char* d = std::getenv("UFC_LEAN_DEPTH")) depth = std::atoi(d);
-    if (const char* ab = std::getenv("UFC_LEAN_ABL")) abl = std::atoi(ab);
-    if (const char* sc = std::getenv("UFC_LEAN_SCHED")) sched = std::atoi(sc);
-  }
-#endif
-#ifdef UFC_TUNING
-  if (const char* wv = std::getenv("UFC_LEAN_WAVES")) waves = std::atoi(wv);  // A/B: 8 or 16
-  // A/B of the main loop's loads: UFC_LEAN_LOADV=skip:first:mid:last (frame_crc.hip lean_loadv)
-  if (const char* lv = std::getenv("UFC_LEAN_LOADV")) {
-    int sk = 0, f = 0, m = 0, l = 0;
-    if (std::sscanf(lv, "%d:%d:%d:%d", &sk, &f, &m, &l) == 4) abl = 100000 + (sk | f << 1 | m << 6 | l << 11);
-  }
-#endif
+  const int depth = ufc_dev::kLeanDepthDefault, abl = 0, waves = ufc_dev::kLeanWavesDefault;
+  const int sched = ufc_dev::kLeanSchedDefault;
   const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl, sched, waves);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain;
@@ -196,9 +175,6 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
     c.front_ok = (f0 > 0 || front_ok) ? 1u : 0u;
-#ifdef UFC_TUNING
-    if (std::getenv("UFC_FRONT_OK")) c.front_ok = 1u;  // A/B only: the caller guarantees readable pad bytes
-#endif
     // Claim counters: one slot of the ring per launch (zero on entry, reset by the kernel).
     const uint32_t slot = ctx->ctr_seq.fetch_add(1) % kCtrSlots;
     c.ctr = ctx->d_ctr + (size_t)slot * ctx->ncu * ufc_dev::kCtrWordsPerBlock;
@@ -206,135 +182,31 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
     uint64_t blocks = (nsets + waves_per_block - 1) / waves_per_block;
     if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
     if (blocks < 1) blocks = 1;
-#ifdef UFC_TUNING
-    // UFC_DBG_WAVES=<file>: per-wave timestamps of this launch (synchronous; tuning only).
-    const char* dbg_path = std::getenv("UFC_DBG_WAVES");
-    unsigned long long* d_dbg = nullptr;
-    if (dbg_path && hipMalloc(&d_dbg, blocks * waves_per_block * 32) == hipSuccess) c.dbg = d_dbg;
-#endif
     void* args[] = {&c};
     hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
-#ifdef UFC_TUNING
-    if (d_dbg) {
-      std::vector<unsigned long long> h(blocks * waves_per_block * 4);
-      (void)hipStreamSynchronize(stream);
-      (void)hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost);
-      (void)hipFree(d_dbg);
-      if (FILE* f = std::fopen(dbg_path, "wb")) {
-        std::fwrite(h.data(), 8, h.size(), f);
-        std::fclose(f);
-      }
-    }
-#endif
   }
   return UFC_OK;
 }
 
-#ifdef UFC_TUNING
-int launch_lean_varlen(ufc_ctx* ctx, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream, bool pairs = false) {
-  // Claimed sets, 16 waves: measured fastest for mixed lengths (compute-heavy per set; DESIGN.md
-  // section 5.2).  UFC_VARLEN_BLOCKED8: the static blocked schedule at 8 waves (A/B).
-  int abl = 0, sched = ufc_dev::kSchedClaim, waves = 16;
-  if (ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_BLOCKED8) {
-    sched = ufc_dev::kSchedBlocked;
-    waves = 8;
-  }
-  // UFC_VARLEN_SORTED (the default): frames sorted by block count within runs of 64
-  // (ufc_dev::sort_runs) first, default-policy loads (config 3: 1.86 ms against 1.98 ms for the
-  // claimed unsorted sets).
-  bool sorted = ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_SORTED || ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_AUTO;
-  // (AUTO lands here only when the 8-lane kernel does not apply)
-#ifdef UFC_TUNING
-  if (const char* ab = std::getenv("UFC_VL_ABL")) abl = std::atoi(ab);
-  if (const char* sc = std::getenv("UFC_VL_SCHED")) sched = std::atoi(sc);
-  if (const char* wv = std::getenv("UFC_VL_WAVES")) waves = std::atoi(wv);
-#endif
-  if (sorted && !(sched == ufc_dev::kSchedClaim && waves == 16)) sorted = false;
-  const void* fn = ufc_dev::varlen_kernel_symbol(seal, pairs, pairs ? 0 : abl, sched, waves, sorted);
-  if (!fn) return UFC_ERR_INVALID_ARG;
-  kp.chain_tab = ctx->d_chain;
-  kp.nib_img = ctx->d_nib;
-  kp.G = ctx->G;
-  // Offsets stay absolute (relative to kp.bytes) in every chunk; a chunk only shifts the offsets
-  // and output pointers.  Chunks keep set indices below 2^30.
-  const uint64_t waves_per_block = (uint64_t)waves;
-  // (sorted: recorded frame indices stay below 2^30)
-  const uint64_t chunk = sorted ? (uint64_t)1 << 29 : (uint64_t)1 << 31;
-  const uint64_t total = kp.nframes;
-  hipError_t e;
-  void* rec = nullptr;
-  if (sorted) {
-    const size_t need = (size_t)((std::min(chunk, total) + 63) / 64 * 64) * 16;
-    if ((e = stream_scratch(ctx, kScratchSortRec, stream, need, &rec)) != hipSuccess) return hip_fail(ctx, e);
-  }
-  for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
-    ufc_dev::KernelParams c = kp;
-    c.nframes = std::min(chunk, total - f0);
-    c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
-    if (sorted) {
-      if ((e = (hipError_t)ufc_dev::sort_runs(c.offsets, pairs, c.nframes, rec, stream)) != hipSuccess)
-        return hip_fail(ctx, e);
-      c.offsets_csr = pairs ? nullptr : c.offsets;
-      c.offsets = (const uint64_t*)rec;
-    }
-    if (kp.crc_out) c.crc_out = kp.crc_out + f0;
-    if (kp.valid_out) c.valid_out = kp.valid_out + f0;
-    const uint32_t slot = ctx->ctr_seq.fetch_add(1) % kCtrSlots;
-    c.ctr = ctx->d_ctr + (size_t)slot * ctx->ncu * ufc_dev::kCtrWordsPerBlock;
-    const uint64_t nsets = (c.nframes + 3) / 4;
-    uint64_t blocks = (nsets + waves_per_block * 4 - 1) / (waves_per_block * 4);
-    if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
-    if (blocks < 1) blocks = 1;
-    void* args[] = {&c};
-    e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
-  }
-  return UFC_OK;
-}
-#endif  // UFC_TUNING
 
 // The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): one launch per chunk of
-// < 2^29 frames, each run of 64 frames sorted by block count inside the kernel (tuning builds: the
-// sort_runs pre-pass into per-stream scratch instead, UFC_V8_PRESORT=1).  Any
-// buffer size: each set's loads are relative to the set's own base (a set whose frames lie
-// 2 GB or more apart, possible with pairs, runs on the kernel's byte path).
+// < 2^29 frames, each run of 64 frames sorted by piece count inside the kernel.  Any buffer size:
+// each set's loads are relative to its run's own base (a set whose frames lie 2 GB or more apart,
+// possible with pairs, runs on the kernel's byte path).
 int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  bool insort = true;  // runs sorted inside the kernel; UFC_V8_PRESORT=1 (tuning): the sort_runs pre-pass
-#ifdef UFC_TUNING
-  if (const char* ps = std::getenv("UFC_V8_PRESORT")) insort = std::atoi(ps) == 0;
-#endif
-  const int waves = 12;
-  int sortw = 64, aux = 0;  // runs sorted whole, default-policy loads; UFC_V8_SORTW / UFC_V8_AUX (tuning): A/B
-  bool geor = true;         // per-run geometry (product); UFC_V8_GEOR=0 (tuning): per-set geometry
-#ifdef UFC_TUNING
-  if (const char* sw = std::getenv("UFC_V8_SORTW")) sortw = std::atoi(sw);
-  if (const char* ax = std::getenv("UFC_V8_AUX")) aux = std::atoi(ax);
-  if (const char* gr = std::getenv("UFC_V8_GEOR")) geor = std::atoi(gr) != 0;
-#endif
-  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs, insort, sortw, aux, geor);
+  const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs);
   if (!fn) return UFC_ERR_INVALID_ARG;
+  const int waves = ufc_dev::varlen8_waves();
   kp.chain_tab = ctx->d_chain128;
   kp.nib_img = ctx->d_nib32;
   kp.G = ctx->G;
   const uint64_t chunk = (uint64_t)1 << 29;  // (32-bit set indices: 8 per run of 64 frames)
   const uint64_t total = kp.nframes;
-  hipError_t e;
-  void* rec = nullptr;
-  if (!insort) {
-    const size_t need = (size_t)((std::min(chunk, total) + 63) / 64 * 64) * 16;
-    if ((e = stream_scratch(ctx, kScratchSortRec, stream, need, &rec)) != hipSuccess) return hip_fail(ctx, e);
-  }
   for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
     c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
-    c.offsets_csr = pairs ? nullptr : c.offsets;
-    if (!insort) {
-      if ((e = (hipError_t)ufc_dev::sort_runs(c.offsets, pairs, c.nframes, rec, stream)) != hipSuccess)
-        return hip_fail(ctx, e);
-      c.offsets = (const uint64_t*)rec;
-    }
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
     // one workgroup per CU, at least one run of 64 frames per wave
@@ -342,33 +214,12 @@ int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& k
     uint64_t blocks = (nruns + waves - 1) / waves;
     if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
     if (blocks < 1) blocks = 1;
-#ifdef UFC_TUNING
-    const char* dbg_path = std::getenv("UFC_DBG_WAVES");  // per-wave timestamps (synchronous; tuning only)
-    unsigned long long* d_dbg = nullptr;
-    if (dbg_path && hipMalloc(&d_dbg, blocks * waves * 32) == hipSuccess) c.dbg = d_dbg;
-#endif
     void* args[] = {&c};
-    e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
+    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
     if (e != hipSuccess) return hip_fail(ctx, e);
-#ifdef UFC_TUNING
-    if (d_dbg) {
-      std::vector<unsigned long long> h(blocks * waves * 4);
-      (void)hipStreamSynchronize(stream);
-      (void)hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost);
-      (void)hipFree(d_dbg);
-      if (FILE* f = std::fopen(dbg_path, "wb")) {
-        std::fwrite(h.data(), 8, h.size(), f);
-        std::fclose(f);
-      }
-    }
-#endif
   }
   return UFC_OK;
 }
-
-// Variable-length batches: the sorted-runs kernel by default; the claimed 16-wave and blocked 8-wave
-// schedules, the block-stream kernel and the generic kernel by option.
-int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream);
 
 // Kernel configuration and mode bits for a fixed frame length: J = 256-byte blocks per frame.
 Config fixed_config(const ufc_ctx* ctx, uint64_t frame_len, int* freeze) {
@@ -387,19 +238,11 @@ Config varlen_config(const ufc_ctx* ctx) {
   return Config{ufc_dev::config_available(jc) ? jc : 3};
 }
 
+// Variable-length batches: the sorted-runs 8-lane kernel; the generic kernel by option (CSR only).
 int launch_varlen_any(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
-  const int opt = ctx->opt[UFC_OPT_VARLEN_KERNEL];
-  if (opt == UFC_VARLEN_SORTED8 || opt == UFC_VARLEN_AUTO) {
-    const int rc = launch_varlen8(ctx, seal, pairs, kp, stream);
-    if (rc != UFC_ERR_INVALID_ARG) return rc;  // (not applicable: the 4-lane kernel below)
-  }
-  if (opt == UFC_VARLEN_GENERIC && !pairs)
+  if (ctx->opt[UFC_OPT_VARLEN_KERNEL] == UFC_VARLEN_GENERIC && !pairs)
     return launch(ctx, varlen_config(ctx), ufc_dev::kModeVarlen | (seal ? ufc_dev::kModeSeal : 0), kp, stream);
-#ifdef UFC_TUNING
-  return launch_lean_varlen(ctx, seal, kp, stream, pairs);
-#else
-  return launch_varlen8(ctx, seal, pairs, kp, stream);  // (pairs under UFC_VARLEN_GENERIC)
-#endif
+  return launch_varlen8(ctx, seal, pairs, kp, stream);
 }
 
 using ufc_internal::kMaxFrameLen;
@@ -462,18 +305,11 @@ int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value) {
   if (!ctx || option < 0 || option >= UFC_OPT_COUNT_) return UFC_ERR_INVALID_ARG;
   switch (option) {
     case UFC_OPT_FIXED_KERNEL:
-      if (value < UFC_FIXED_AUTO || value > UFC_FIXED_CLAIM16) return UFC_ERR_INVALID_ARG;
-#ifndef UFC_TUNING
-      if (value == UFC_FIXED_CLAIM16) return UFC_ERR_INVALID_ARG;  // (A/B kernel of tuning builds)
-#endif
+      if (value != UFC_FIXED_AUTO && value != UFC_FIXED_GENERIC) return UFC_ERR_INVALID_ARG;
       break;
     case UFC_OPT_VARLEN_KERNEL:
-      if (value < UFC_VARLEN_AUTO || value > UFC_VARLEN_STREAM) return UFC_ERR_INVALID_ARG;
-      if (value == UFC_VARLEN_BLOCKSTREAM || value == UFC_VARLEN_STREAM) return UFC_ERR_INVALID_ARG;  // (removed)
-#ifndef UFC_TUNING
       if (value != UFC_VARLEN_AUTO && value != UFC_VARLEN_GENERIC && value != UFC_VARLEN_SORTED8)
-        return UFC_ERR_INVALID_ARG;  // (round-1 and block-stream kernels: A/B in tuning builds)
-#endif
+        return UFC_ERR_INVALID_ARG;
       break;
     case UFC_OPT_GENERIC_JC:
       if (value != 0 && !ufc_dev::config_available(value)) return UFC_ERR_INVALID_ARG;
@@ -512,6 +348,7 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
   ufc::build_chain_table(chain128.data(), 128);
   ufc::build_nibble_image32(nib32.data());
   ctx->G = ufc::init_prefix_word();
+  ctx->opt[UFC_OPT_SEAL_KERNEL] = UFC_SEAL_INLINE;  // (the other options default to 0)
   hipError_t e;
   if ((e = hipMalloc(&ctx->d_chain, chain.size() * 4)) != hipSuccess ||
       (e = hipMalloc(&ctx->d_nib, nib.size() * 4)) != hipSuccess ||
@@ -528,21 +365,6 @@ int ufc_ctx_create(ufc_ctx** out, int device) {
     return UFC_ERR_HIP;
   }
   // The kernels declare their 160 KiB of LDS statically: no dynamic-LDS attribute to set.
-#ifdef UFC_TUNING
-  // Tuning builds: the A/B scripts select kernels through the environment (read once, here).
-  if (const char* k = std::getenv("UFC_FIXED_KERNEL"))
-    ctx->opt[UFC_OPT_FIXED_KERNEL] = std::strcmp(k, "generic") == 0 ? UFC_FIXED_GENERIC
-                                     : std::strcmp(k, "claim16") == 0 ? UFC_FIXED_CLAIM16 : UFC_FIXED_AUTO;
-  if (const char* k = std::getenv("UFC_VARLEN_KERNEL"))
-    ctx->opt[UFC_OPT_VARLEN_KERNEL] = std::strcmp(k, "generic") == 0 ? UFC_VARLEN_GENERIC
-                                      : std::strcmp(k, "sorted") == 0 ? UFC_VARLEN_SORTED
-                                      : std::strcmp(k, "blocked8") == 0 ? UFC_VARLEN_BLOCKED8
-                                      : std::strcmp(k, "claim16") == 0 ? UFC_VARLEN_CLAIM16
-                                      : std::strcmp(k, "sorted8") == 0 ? UFC_VARLEN_SORTED8 : UFC_VARLEN_AUTO;
-  if (const char* j = std::getenv("UFC_FIXED_JC")) ctx->opt[UFC_OPT_GENERIC_JC] = std::atoi(j);
-  if (const char* k = std::getenv("UFC_SEAL_KERNEL"))
-    ctx->opt[UFC_OPT_SEAL_KERNEL] = std::strcmp(k, "two_pass") == 0 ? UFC_SEAL_TWO_PASS : UFC_SEAL_INLINE;
-#endif
   *out = ctx;
   return UFC_OK;
 }
@@ -632,12 +454,6 @@ int ufc_internal::crc_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride
   int freeze;
   const Config cfg = fixed_config(ctx, frame_len, &freeze);
   int lean = lean_fixed_blocks(ctx, frame_len, stride, n);
-#ifdef UFC_TUNING
-  if (const char* ab = std::getenv("UFC_ABLATE")) {
-    freeze |= std::atoi(ab);
-    lean = 0;
-  }
-#endif
   ufc_dev::KernelParams kp{};
   kp.bytes = d_frames;
   kp.stride = stride;

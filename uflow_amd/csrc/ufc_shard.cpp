@@ -94,6 +94,9 @@ constexpr int kChunkFramesLog2 = 22;
 
 }  // namespace
 
+// How long a sharded call waits for every peer to join its status agreement (ufc_comm_set_timeout).
+constexpr int kDefaultTimeoutMs = 60000;
+
 struct ufc_comm {
   ufc_ctx* ctx = nullptr;
   int nranks = 0;
@@ -107,7 +110,9 @@ struct ufc_comm {
   int32_t* d_status = nullptr;
   int32_t* h_status = nullptr;  // [0] this rank's status, [1] the agreed (max over ranks)
   int last_nccl_error = 0;
-  bool broken = false;  // aborted after a rank-local failure mid-gather: every later call fails
+  bool broken = false;   // aborted after a rank-local failure mid-gather, or stalled: every later call fails
+  bool stalled = false;  // a peer missed the status agreement's deadline: the all-reduce is still pending
+  int timeout_ms = kDefaultTimeoutMs;  // the status agreement's deadline (0: wait for ever)
   hipEvent_t ev[kMaxChunks] = {};
 };
 
@@ -183,9 +188,13 @@ int abort_comm(ufc_comm* comm, int rc) {
 // Every rank's verdict on its own arguments, agreed before any transfer is queued: a one-word
 // max-all-reduce on the control communicator, read back through pinned memory.  A rank-local failure
 // (a missing shard pointer) then fails the call on every rank -- UFC_ERR_PEER on the others -- and
-// the communicator stays usable.  The wait polls the stream and the control communicator's
-// asynchronous error (a peer that never makes the call is left to the caller's supervision: RCCL's
-// abort measured not to return while that peer's side of the all-reduce is missing).
+// the communicator stays usable.  The host waits here for every peer to make the call (so every
+// sharded call blocks its thread until then), polling the stream and the control communicator's
+// asynchronous error, up to the communicator's deadline (ufc_comm_set_timeout).  A peer that has not
+// joined by then fails the call with UFC_ERR_COMM and leaves the communicator stalled: nothing is
+// aborted (ncclCommAbort measured not to return while the peer's side of the all-reduce is missing),
+// the pending all-reduce and its buffers stay as they are, every later call returns UFC_ERR_COMM, and
+// the caller ends the process (teardown at process exit).
 // UFC_SHARD_TRACE=1: progress of the status agreement on stderr (diagnosing a peer that never joins).
 bool shard_trace() {
   static const bool on = [] {
@@ -207,6 +216,7 @@ bool shard_trace() {
 int agree_status(ufc_comm* comm, int local_rc) {
   if (comm->nranks == 1) return local_rc;
   const Rccl& r = rccl();
+  DeviceGuard g(ufc_internal::ctx_device(comm->ctx));  // (the control stream's device, whatever the caller's)
   UFC_TRACE("agree_status: local %d, enqueueing", local_rc);
   comm->h_status[0] = local_rc != UFC_OK ? 1 : 0;
   comm->h_status[1] = -1;
@@ -224,6 +234,7 @@ int agree_status(ufc_comm* comm, int local_rc) {
     ufc_internal::note_hip_error(comm->ctx, (int)e);
     return abort_comm(comm, UFC_ERR_HIP);
   }
+  const auto t0 = std::chrono::steady_clock::now();
   for (int spin = 0;; spin++) {
     e = hipStreamQuery(comm->ctl_stream);
     if (e == hipSuccess) break;
@@ -234,6 +245,13 @@ int agree_status(ufc_comm* comm, int local_rc) {
     ncclResult_t ae = ncclSuccess;
     if (r.CommGetAsyncError(comm->ctl, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress)
       return abort_comm(comm, nccl_fail(comm, ae));
+    if (comm->timeout_ms > 0 && (spin & 63) == 0 &&
+        std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(comm->timeout_ms)) {
+      UFC_TRACE("agree_status: no answer from every peer in %d ms: stalled", comm->timeout_ms);
+      comm->stalled = true;
+      comm->broken = true;
+      return UFC_ERR_COMM;
+    }
     if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(spin > 20000 ? 1000 : 20));
   }
   UFC_TRACE("agree_status: agreed %d", comm->h_status[1]);
@@ -469,6 +487,13 @@ int ufc_comm_create(ufc_comm** out, ufc_ctx* ctx, int nranks, int rank, const ui
 
 int ufc_comm_destroy(ufc_comm* comm) {
   if (!comm) return UFC_OK;
+  if (comm->stalled) {
+    // The status all-reduce is still pending on the control stream (a peer never joined): destroying
+    // the communicators, the stream or the status words could wait for it or free what it writes.
+    // Everything is left to process exit; the handle is gone.
+    delete comm;
+    return UFC_ERR_COMM;
+  }
   {
     DeviceGuard g(ufc_internal::ctx_device(comm->ctx));
     if (comm->ctl) (void)rccl().CommDestroy(comm->ctl);
@@ -480,6 +505,12 @@ int ufc_comm_destroy(ufc_comm* comm) {
     if (comm->h_status) (void)hipHostFree(comm->h_status);
   }
   delete comm;
+  return UFC_OK;
+}
+
+int ufc_comm_set_timeout(ufc_comm* comm, int timeout_ms) {
+  if (!comm || timeout_ms < 0) return UFC_ERR_INVALID_ARG;
+  comm->timeout_ms = timeout_ms;
   return UFC_OK;
 }
 

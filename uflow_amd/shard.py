@@ -108,6 +108,11 @@ class ShardedGate:
             lib().ufc_comm_destroy(self._comm)
             self._comm = ctypes.c_void_p()
 
+    def set_timeout(self, timeout_ms):
+        """How long a sharded call waits for every peer to join it (ufc_comm_set_timeout): past it the
+        call raises NativeError(UFC_ERR_COMM) and the communicator is stalled for good."""
+        check(lib().ufc_comm_set_timeout(self._comm, int(timeout_ms)), "ufc_comm_set_timeout")
+
     def __del__(self):
         try:
             self.close()
