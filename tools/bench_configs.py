@@ -237,9 +237,22 @@ def parse(eng, dev, reps, n=1_000_000):
     k = int(used.cpu()[0])
     # (a checksum of the item records and infos: equal across A/B variants)
     digest = int(items[:k].view(torch.int64).sum()) ^ int(infos.view(torch.int64).sum())
-    return {"config": "f3: device parse (count, scan, fill) of 1M uflow frames after the gate", "frames": n,
+    # the gate and the parse back to back (Frame::read end to end: serial/mod.rs:675-706)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def both():
+        eng.crc_varlen(d, o, crc_out=crc, valid_out=valid)
+        eng.parse_varlen(d, o, valid, items_cap=cap)
+    settle(both, 300)
+    med2, _ = timed(both, reps)
+    # algorithmic bytes of the parse: the frame bytes read once, the offsets and
+    # gate flags read, the 24-byte items and 32-byte infos written
+    algo = total + 8 * (n + 1) + n + 24 * k + 32 * n
+    return {"config": "f3: device parse of 1M uflow frames after the gate", "frames": n,
             "frame_bytes": total, "items": k, "items_digest": digest, "ms": round(med, 4), "mean_ms": round(mean, 4),
-            "frames_per_s": round(n / med * 1e3), "GB_s_of_frame_bytes": round(total / med / 1e-3 / 1e9, 1)}
+            "frames_per_s": round(n / med * 1e3), "GB_s_of_frame_bytes": round(total / med / 1e-3 / 1e9, 1),
+            "algorithmic_bytes": algo, "frac_of_8TBs": round(algo / (med * 1e-3) / 8e12, 4),
+            "gate_plus_parse_ms": round(med2, 4)}
 
 
 def host(eng, reps=5, n=1_000_000, L=1472):
@@ -254,17 +267,21 @@ def host(eng, reps=5, n=1_000_000, L=1472):
         a = t.numpy()
         a[np.arange(0, n, 500) * L + 9] ^= 0x40
         offsets = (np.arange(n + 1, dtype=np.uint64) * L)
-        eng.validate_host_varlen(a, offsets)  # warm (staging allocation)
-        times = []
-        for _ in range(reps):
-            t0 = time.perf_counter()
-            crc, valid = eng.validate_host_varlen(a, offsets)
-            times.append(time.perf_counter() - t0)
-        sec = float(np.median(times))
-        ok = int(valid.sum()) == n - len(range(0, n, 500))
-        res.append({"config": f"5 (GPU leg): host-resident {n} x {L}-B frames, {kind} buffer, H2D + CRC + D2H",
-                    "frames": n, "seconds": round(sec, 5), "GiB_s": round(n * L / sec / 2**30, 2),
-                    "frames_per_s": round(n / sec), "valid_ok": ok})
+        lens = np.full(n, L, dtype=np.uint32)
+        for entry, fn in (("ufc_validate_host_varlen (CSR)", lambda: eng.validate_host_varlen(a, offsets)),
+                          ("ufc_validate_host_slots (recvmmsg slots, stride 1472)",
+                           lambda: eng.validate_host_slots(a, L, lens))):
+            fn()  # warm (staging allocation)
+            times = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                crc, valid = fn()
+                times.append(time.perf_counter() - t0)
+            sec = float(np.median(times))
+            ok = int(valid.sum()) == n - len(range(0, n, 500))
+            res.append({"config": f"5 (GPU leg): host-resident {n} x {L}-B frames, {kind} buffer, H2D + CRC + D2H",
+                        "entry": entry, "frames": n, "seconds": round(sec, 5), "GiB_s": round(n * L / sec / 2**30, 2),
+                        "frames_per_s": round(n / sec), "valid_ok": ok})
     return res
 
 

@@ -1,0 +1,47 @@
+"""Build an experiment variant of libuflowcrc.so into abl/<name>.so: the product sources copied to a
+scratch tree, `file:old=>new` substitutions applied (each must match), compiled with the product's
+flags.  A/B measurement only (tools/ab_inproc.py); the product library is never touched.
+Usage: python tools/build_variant.py <name> 'frame_crc_varlen8.hip:old=>new' ..."""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+from concurrent.futures import ThreadPoolExecutor
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+from uflow_amd import _build  # noqa: E402
+
+
+def main():
+    name, subs = sys.argv[1], sys.argv[2:]
+    d = tempfile.mkdtemp(prefix="ufc_var_")
+    shutil.copytree(os.path.join(REPO, "uflow_amd", "csrc"), os.path.join(d, "uflow_amd", "csrc"))
+    shutil.copytree(os.path.join(REPO, "include"), os.path.join(d, "include"))
+    for sub in subs:
+        fn, rest = sub.split(":", 1)
+        old, new = rest.split("=>", 1)
+        p = os.path.join(d, "uflow_amd", "csrc", fn)
+        s = open(p).read()
+        assert old in s, f"{fn}: no match for {old!r}"
+        open(p, "w").write(s.replace(old, new))
+    sources, flags, _ = _build._native_identity()
+    objs = []
+    jobs = []
+    for src in sources:
+        obj = os.path.join(d, src + ".o")
+        objs.append(obj)
+        jobs.append(flags + ["-c", os.path.join(d, "uflow_amd", "csrc", src), "-o", obj])
+    with ThreadPoolExecutor(8) as ex:
+        rcs = list(ex.map(lambda c: subprocess.run(c).returncode, jobs))
+    assert not any(rcs), rcs
+    os.makedirs(os.path.join(REPO, "abl"), exist_ok=True)
+    out = os.path.join(REPO, "abl", name + ".so")
+    subprocess.run([_build.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs + ["-ldl"], check=True)
+    shutil.rmtree(d)
+    print(out)
+
+
+if __name__ == "__main__":
+    main()

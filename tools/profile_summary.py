@@ -1,6 +1,7 @@
-"""profiles/ from a tools/profile_workloads.sh run: copies every workload's kernel-trace stats and
-counter CSVs as profiles/<prefix>_<workload>_{kernel_stats,kernel_trace_dur,pmc_fetch,pmc_write}.*,
-and writes (merges into) profiles/<prefix>_summary.json: per workload, the kernel(s) it times, the average and
+"""profiles/ from a tools/profile_workloads.sh run: copies every workload's kernel-trace stats as
+profiles/<prefix>_<workload>_kernel_stats.csv (the raw per-dispatch counter CSVs stay under
+gpurun_out/<tag>/, untracked: rerun tools/profile_workloads.sh <tag> to regenerate them), and writes
+(merges into) profiles/<prefix>_summary.json: per workload, the kernel(s) it times, the average and
 median dispatch duration from the trace (warm dispatches only), the algorithmic bytes per dispatch,
 the roofline fraction recomputed from them, and FETCH/WRITE bytes per dispatch (FETCH_SIZE KiB x1024
 x2, the gfx950 correction of MI355X_MICROARCH.md; WRITE_SIZE KiB x1024).  Also regenerates
@@ -68,11 +69,6 @@ def main():
             for root, _, files in os.walk(kt):
                 if sfx in files:
                     shutil.copy(os.path.join(root, sfx), os.path.join(dst, f"{prefix}_{w}_{name}"))
-        for kind in ("fetch", "write"):
-            for root, _, files in os.walk(os.path.join(src, f"{w}_{kind}")):
-                for fn in files:
-                    if fn.endswith("counter_collection.csv"):
-                        shutil.copy(os.path.join(root, fn), os.path.join(dst, f"{prefix}_{w}_pmc_{kind}.csv"))
         line = last_json(os.path.join(src, f"{w}_ktrace.log"))
         trace = None
         for root, _, files in os.walk(kt):
@@ -120,7 +116,8 @@ def main():
                "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of `python3 bench.py "
                          "--steps 5 --warmup 2 --no-cpu-baseline --settle-ms 50 --no-ceiling` "
                          "(tools/profile_workloads.sh); FETCH_SIZE KiB x1024 x2 (gfx950 half-count correction, "
-                         f"MI355X_MICROARCH.md HBM section), WRITE_SIZE KiB x1024; raw CSVs in profiles/{prefix}_bench_pmc_*.csv"}
+                         f"MI355X_MICROARCH.md HBM section), WRITE_SIZE KiB x1024; raw CSVs: gpurun_out/{tag}/bench_{{fetch,write}} "
+                         "(untracked; tools/profile_workloads.sh regenerates them)"}
         with open(os.path.join(dst, "pmc_traffic.json"), "w") as f:
             json.dump(out, f, indent=1)
     print(json.dumps(summary, indent=1))

@@ -72,13 +72,15 @@ struct DevBytes {
 // failing at random, profiles/EXPERIMENTS.md).
 typedef unsigned int u32x4_h __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1), aligned(1))) u32x4_h g_u32x4_h;
+template <uint32_t HEAD = 16>
 struct DevBytesHead {
+  static_assert(HEAD == 16 || HEAD == 8, "head bytes");
   const uint8_t* p;
   uint64_t w0, w1;  // bytes 0..7 and 8..15, little-endian
   uint32_t held;    // bytes 0 .. held-1 in w0/w1: 16, 8 or 0
   __device__ static DevBytesHead load(const uint8_t* q, uint32_t len) {  // (any byte address: unaligned access mode)
     DevBytesHead r{q, 0ull, 0ull, 0u};
-    if (len >= 16) {
+    if (HEAD == 16 && len >= 16) {
       const u32x4_h v = *(g_u32x4_h*)q;
       r.w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
       r.w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
@@ -271,7 +273,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
-    const DevBytesHead rd = DevBytesHead::load(bytes + a, len);
+    const DevBytesHead<16> rd = DevBytesHead<16>::load(bytes + a, len);
     const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
     const uint32_t cnt = ok ? info.item_count : 0u;
@@ -473,6 +475,204 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
   }
 }
 
+// ---- One-pass parse (round 5): walk, item scan and emit in one kernel ----
+// Each workgroup takes the next tile of 256 frames from a launch counter (so tiles start in order),
+// walks them (one thread per frame, header offsets in LDS: 16 inline slots per frame, then 16-slot
+// chunks of a workgroup pool, at most 7 per frame), scans its item counts, learns its first item from
+// its predecessors by decoupled look-back (one 8-byte word per tile: flag | count, agent-scope relaxed
+// atomic stores and polls, MI355X_MICROARCH.md's granule hand-off), writes each frame's info once
+// with its item_first, and emits its items at once: item-parallel, each header read again while the
+// lines the walk just read are still in the caches -- no header slots through memory, no scan launch,
+// no second pass over the batch from HBM.  The walk reads each frame's first 8 bytes in one load
+// (the 16-byte head stays out until the cause of its round-4 failures is shown).
+constexpr uint32_t kFusedInline = 16;
+constexpr uint32_t kFusedChunk = 16;
+constexpr uint32_t kFusedPoolChunks = 128;
+constexpr uint32_t kFusedMaxChunks = 7;  // 16 + 7 * 16 = 128 > the 127 datagrams of a data frame
+constexpr uint64_t kLbAggregate = 1ull << 62, kLbPrefix = 1ull << 63, kLbValue = kLbAggregate - 1;
+
+struct ChunkSink {
+  static constexpr bool kDecode = false;
+  uint16_t* inl;      // this thread's inline slots (slot k at k * kParseThreads)
+  uint16_t* pool;     // the workgroup's pool of chunks
+  uint32_t* pctr;     // its chunk counter
+  uint8_t* cids;      // this thread's chunk ids (chunk c at c * kParseThreads)
+  bool* full;
+  __device__ bool on() const { return true; }
+  __device__ void operator()(uint32_t, const ufc_item&) const {}
+  __device__ void header(uint32_t k, uint32_t off) const {
+    if (k < kFusedInline) {
+      inl[k * kParseThreads] = (uint16_t)off;
+      return;
+    }
+    if (*full) return;
+    const uint32_t kk = k - kFusedInline, c = kk / kFusedChunk;
+    if (kk % kFusedChunk == 0) {
+      const uint32_t id = c < kFusedMaxChunks ? atomicAdd(pctr, 1u) : kFusedPoolChunks;  // (LDS atomic)
+      if (id >= kFusedPoolChunks) {
+        *full = true;
+        return;
+      }
+      cids[c * kParseThreads] = (uint8_t)id;
+    }
+    pool[cids[c * kParseThreads] * kFusedChunk + kk % kFusedChunk] = (uint16_t)off;
+  }
+};
+
+__global__ __launch_bounds__(kParseThreads) void parse_fused_kernel(const uint8_t* bytes, const uint64_t* offsets,
+                                                                    uint64_t n, const uint8_t* valid,
+                                                                    ufc_frame_info* infos, ufc_item* items,
+                                                                    uint64_t cap, uint64_t* items_used,
+                                                                    uint32_t* tile_ctr, uint64_t* lb) {
+  __shared__ uint16_t inl[kFusedInline * kParseThreads];
+  __shared__ uint16_t pool[kFusedPoolChunks * kFusedChunk];
+  __shared__ uint8_t cids[kFusedMaxChunks * kParseThreads];
+  __shared__ uint32_t lfirst[kParseThreads];
+  __shared__ uint64_t lstart[kParseThreads];
+  __shared__ uint8_t lmode[kParseThreads];
+  __shared__ typename BlockScan::TempStorage scan_tmp;
+  __shared__ uint32_t s_tile, s_pctr, s_end;
+  __shared__ uint64_t s_base;
+  const uint32_t t = threadIdx.x;
+  if (t == 0) {
+    s_tile = atomicAdd(tile_ctr, 1u);  // tiles start in claim order: every lower tile has started
+    s_pctr = 0;
+  }
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t i0 = tile * kParseThreads, i = i0 + t;
+  const uint32_t nb = (uint32_t)min((uint64_t)kParseThreads, n - i0);  // frames of this tile
+  uint32_t cnt = 0;
+  uint8_t mode = kItemsNone;
+  uint64_t a = 0;
+  bool full = false;
+  ufc_frame_info info{};
+  if (i < n) {
+    const uint32_t len = frame_len32(offsets, i, a);
+    const DevBytesHead<8> rd = DevBytesHead<8>::load(bytes + a, len);
+    const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
+                                             ChunkSink{inl + t, pool, &s_pctr, cids + t, &full}, kPosSlots * 2);
+    cnt = ok ? info.item_count : 0u;
+    if (cnt) {
+      if (info.kind == UFC_FRAME_ACK)
+        mode = kItemsAck;
+      else if (!full && len <= 0xFFFFu)
+        mode = kItemsPos;
+      else
+        mode = kItemsWalk;
+    }
+  }
+  uint32_t lo, total;
+  BlockScan(scan_tmp).ExclusiveSum(cnt, lo, total);
+  if (t == 0) {  // decoupled look-back over the tiles before this one
+    uint64_t base = 0;
+    if (tile == 0) {
+      __hip_atomic_store(lb, kLbPrefix | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(lb + tile, kLbAggregate | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (uint64_t q = tile - 1;;) {
+        const uint64_t v = __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v & (kLbAggregate | kLbPrefix)) == 0) {
+          __builtin_amdgcn_s_sleep(2);
+          continue;
+        }
+        base += v & kLbValue;
+        if ((v & kLbPrefix) || q == 0) break;
+        q--;
+      }
+      __hip_atomic_store(lb + tile, kLbPrefix | (base + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_base = base;
+    s_end = total;
+  }
+  __syncthreads();
+  const uint64_t wbase = s_base;
+  const uint64_t first = wbase + lo;
+  if (i < n) {
+    info.item_first = (uint32_t)first;
+    infos[i] = info;
+    if (i == n - 1 && items_used) *items_used = first + cnt;
+  }
+  lfirst[t] = lo;
+  lstart[t] = a;
+  lmode[t] = mode;
+  __syncthreads();
+  if (!items) return;
+
+  // Header bytes through a buffer resource over the tile's bytes (as parse_emit_kernel).
+  const uint64_t span_lo = lstart[0];
+  const uint64_t span_hi = offsets[i0 + nb];
+  const uintptr_t base_addr = (uintptr_t)(bytes + span_lo);
+  const uint32_t delta = (uint32_t)(base_addr & 3u);
+  const uint64_t range = (span_hi - span_lo + delta + 3) & ~(uint64_t)3;
+  const bool buf_ok = span_hi >= span_lo && range < 0xFFFFFFF0ull;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(base_addr - delta), 0, buf_ok ? (int)(uint32_t)range : 0, 0x00020000);
+  const uint32_t g_end = (uint32_t)min((uint64_t)s_end, cap > wbase ? cap - wbase : 0ull);
+  for (uint32_t g = t; g < g_end; g += kParseThreads) {
+    uint32_t lo_f = 0, hi_f = nb - 1;  // owner: the last frame whose first item is <= g
+    while (lo_f < hi_f) {
+      const uint32_t mid = (lo_f + hi_f + 1) >> 1;
+      if (lfirst[mid] <= g)
+        lo_f = mid;
+      else
+        hi_f = mid - 1;
+    }
+    const uint32_t f = lo_f, k = g - lfirst[f];
+    const uint8_t m = lmode[f];
+    if (m != kItemsPos && m != kItemsAck) continue;  // (kItemsWalk: the frame's own thread, below)
+    uint32_t hoff;
+    if (m == kItemsAck) {
+      hoff = 1u + ufc_codec::kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
+    } else if (k < kFusedInline) {
+      hoff = inl[k * kParseThreads + f];
+    } else {
+      const uint32_t kk = k - kFusedInline;
+      hoff = pool[cids[(kk / kFusedChunk) * kParseThreads + f] * kFusedChunk + kk % kFusedChunk];
+    }
+    uint32_t w[4];
+    if (buf_ok) {
+      const uint32_t ex = (uint32_t)(lstart[f] - span_lo) + delta + hoff;
+      if (ex + 16 <= (uint32_t)range) {  // one unaligned 16-byte load at the header
+        const u32x4_h v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)ex, 0, 0);
+        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+      } else {  // (a header at the very end of the span: an aligned 16-byte + 4-byte pair)
+        const uint32_t al = ex & ~3u, sh = ex & 3u;
+        const u32x4_h v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)al, 0, 0);
+        const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(al + 16), 0, 0);
+        w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
+        w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
+        w[2] = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
+        w[3] = __builtin_amdgcn_alignbyte(x4, v.w, sh);
+      }
+    } else {
+      const DevBytes rd{bytes + lstart[f] + hoff};
+      for (int q = 0; q < 4; q++) w[q] = 0;
+      const uint32_t nbytes = m == kItemsAck ? UFC_ACK_GROUP_SIZE : 14u;
+      for (uint32_t c = 0; c < nbytes; c++) w[c >> 2] |= rd(c) << (8 * (c & 3));
+    }
+    auto h = [&](uint32_t c) -> uint32_t { return (w[c >> 2] >> (8 * (c & 3))) & 0xFFu; };
+    ufc_item it{};
+    if (m == kItemsPos) {
+      uint32_t hs, dl;
+      ufc_codec::datagram_size(h, hs, dl);
+      ufc_codec::decode_datagram(h, hs, it);
+      it.data_offset = hoff + hs;
+    } else {
+      ufc_codec::decode_ack_group(h, it);
+    }
+    store_item<true>(items + wbase + g, it);
+  }
+  // Frames whose headers did not fit the slots: walked again by their own thread, items stored directly.
+  if (mode == kItemsWalk && first < cap) {
+    uint64_t aa;
+    const uint32_t len = frame_len32(offsets, i, aa);
+    const uint32_t room = (uint32_t)min((uint64_t)cnt, cap - first);
+    ufc_frame_info tmp;
+    ufc_codec::read_frame_to(DevBytes{bytes + aa}, len, valid[i] != 0, tmp, PackedSink{items + first}, room);
+  }
+}
+
 }  // namespace
 
 namespace {
@@ -511,42 +711,15 @@ size_t parse_scratch_bytes(uint64_t n, uint64_t items_cap) {
 hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, hipStream_t stream) {
   const uint64_t n = a.n;
   const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
-  const ParseLayout lay(n, a.items_cap, scan_temp_bytes(n));
-  if (lay.end > scratch_bytes) return hipErrorInvalidValue;
+  // One pass (parse_fused_kernel): a tile counter and one look-back word per tile, zeroed first.
+  const size_t need = 256 + blocks * 8;
+  if (need > scratch_bytes) return hipErrorInvalidValue;
   char* s = (char*)scratch;
-  uint32_t* counts = (uint32_t*)(s + lay.counts);
-  uint32_t* wg_counts = (uint32_t*)(s + lay.wg_counts);
-  uint32_t* wg_firsts = (uint32_t*)(s + lay.wg_firsts);
-  uint8_t* modes = (uint8_t*)(s + lay.modes);
-  unsigned long long* cursor = (unsigned long long*)(s + lay.cursor);
-  uint32_t* bases = (uint32_t*)(s + lay.bases);
-  uint16_t* pos_seg = (uint16_t*)(s + lay.slots);
-  void* temp = s + lay.temp;
-  size_t temp_bytes = lay.end - lay.temp;
-  hipError_t e = hipMemsetAsync(cursor, 0, 8, stream);
+  hipError_t e = hipMemsetAsync(s, 0, need, stream);
   if (e != hipSuccess) return e;
-  bool pool = true;  // pooled header slots (more walking frames per CU); UFC_WALK_POOL=0 (tuning): fixed slots
-  if (pool)
-    parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos,
-                                                                           counts, modes, pos_seg, cursor, bases,
-                                                                           lay.seg_cap, wg_counts);
-  else
-    parse_walk_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
-                                                                      modes, pos_seg, cursor, bases, lay.seg_cap,
-                                                                      wg_counts);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  // each workgroup's first item (the emit adds the frames' own counts within the workgroup)
-  e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, wg_counts, wg_firsts, (int)blocks, stream);
-  if (e != hipSuccess) return e;
-  // One item per thread per round, one non-temporal 16-byte load per header, non-temporal record
-  // stores (0.526 against 0.551 ms with five dword loads; 4 items per round 0.532 with them, 0.543
-  // without; the exact-offset load 0.453 against 0.458 for the aligned pair; non-temporal loads 0.447
-  // against 0.453; non-temporal stores 0.426 against 0.430 on a faster box: DESIGN.md section 5.5).
-  auto emit = parse_emit_kernel<1, 2, kEmitAux, true>;
-  emit<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
-                                                                    wg_firsts, modes, pos_seg, bases, a.items, a.items_cap,
-                                                                    a.items_used);
+  parse_fused_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, a.items,
+                                                                     a.items_cap, a.items_used, (uint32_t*)s,
+                                                                     (uint64_t*)(s + 256));
   return hipGetLastError();
 }
 
