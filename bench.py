@@ -412,6 +412,7 @@ def main():
     gathered = [None, None]  # event on the gather stream after each slot's last gather
     k_step = [0]
     tails = []  # N > 1, timed steps: (compute-stream end, gather-stream end) timing events per step
+    host_call = []  # N > 1, timed steps: host seconds inside ufc_crc_sharded (its blocking status agreement)
 
     def step(ev=None, tail=None):
         i = k_step[0] % len(slots)
@@ -424,7 +425,10 @@ def main():
         if gate is None:
             eng.crc_fixed(frames, L, n=n, crc_out=crc, valid_out=valid)
         else:
+            h0 = time.perf_counter()
             gate.crc_sharded(frames, L, total, crc, valid, root=0, stream=compute, gather_stream=gather)
+            if tail is not None:
+                host_call.append(time.perf_counter() - h0)
             e = torch.cuda.Event(enable_timing=tail is not None)
             e.record(gather)
             gathered[i] = e
@@ -476,8 +480,9 @@ def main():
     split = None
     if sharded:
         tail_ms = float(np.mean([max(0.0, c.elapsed_time(g)) for c, g in tails])) if tails else 0.0
-        mine = torch.tensor([kern_ms, tail_ms], dtype=torch.float64, device=dev)
-        every = [torch.zeros(2, dtype=torch.float64, device=dev) for _ in range(world)]
+        call_ms = float(np.mean(host_call)) * 1e3 if host_call else 0.0
+        mine = torch.tensor([kern_ms, tail_ms, call_ms], dtype=torch.float64, device=dev)
+        every = [torch.zeros(3, dtype=torch.float64, device=dev) for _ in range(world)]
         dist.all_gather(every, mine)
         split = [[float(x) for x in t.cpu()] for t in every]
 
@@ -593,9 +598,13 @@ def main():
         if split is not None:
             result["per_rank_kernel_ms"] = [round(x[0], 4) for x in split]
             result["gather_ms"] = [round(x[1], 4) for x in split]
+            result["host_call_ms"] = [round(x[2], 4) for x in split]
             result["gather_ms_meaning"] = ("per rank and step: how long its gather stream ran past its last "
                                            "gate of the step (HIP events; the RCCL transfer the gates did not "
-                                           "hide); per_rank_kernel_ms: that rank's gates per step")
+                                           "hide); per_rank_kernel_ms: that rank's gates per step; "
+                                           "host_call_ms: host time per step inside ufc_crc_sharded, which "
+                                           "blocks until every peer has joined the call's status agreement "
+                                           "(the gates and transfers themselves are enqueued asynchronously)")
         if n1_ref is not None:
             result["n1_sharded_ref"] = n1_ref
         if ceiling is not None:

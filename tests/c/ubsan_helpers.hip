@@ -2,7 +2,7 @@
 // (-fsanitize=undefined -fno-sanitize-recover=all, tests/test_ubsan_helpers.py), each over its
 // whole argument range and against a byte-wise restatement: an out-of-range shift amount in any arm,
 // selected or not, stops the run ("a mechanical guard against out-of-range shifts").
-//   fix_word, front_fix, data_mask, frame_word_mask, rot_nibble_key  (frame_crc_dev.hpp)
+//   fix_word, front_fix, data_mask, data_mask_bits, frame_word_mask, rot_nibble_key  (frame_crc_dev.hpp)
 //   head_byte                                                        (frame_parse.hpp)
 #include <hip/hip_runtime.h>
 
@@ -81,6 +81,14 @@ int main() {
     CHECK(data_mask(lb) == want, "data_mask(%d) = %08x, want %08x", lb, data_mask(lb), want);
     checks++;
   }
+  // data_mask_bits: b = 8 lb (any int; the varlen gate passes 8 lim - 32 k): the same mask
+  for (int lb = -1000; lb <= 1000; lb++) {
+    const int b = 8 * lb;
+    CHECK(data_mask_bits(b) == data_mask(lb), "data_mask_bits(%d) = %08x, want %08x", b, data_mask_bits(b), data_mask(lb));
+    checks++;
+  }
+  for (int b : {-2147483647 - 1, -2147483647, 2147483647, 33, 31, -1})
+    CHECK(data_mask_bits(b) == (b >= 32 ? ~0u : (b <= 0 ? 0u : ~(0xFFFFFFFFu << b))), "data_mask_bits(%d)", b);
   // frame_word_mask: ob = frame offset of the word's first byte, every frame length 0..2100
   for (uint32_t len = 0; len <= 2100; len++)
     for (int ob = -300; ob <= 2400; ob++) {

@@ -59,5 +59,6 @@ def test_bench_two_ranks_one_device():
     # the N > 1 line separates the gates from the gather
     assert len(j["per_rank_kernel_ms"]) == 2 and all(x > 0 for x in j["per_rank_kernel_ms"])
     assert len(j["gather_ms"]) == 2 and all(x >= 0 for x in j["gather_ms"])
+    assert len(j["host_call_ms"]) == 2 and all(x > 0 for x in j["host_call_ms"])
     ref = j["n1_sharded_ref"]
     assert ref["value"] > 0 and ref["frames"] > 0 and ref["valid_flags_as_planted"]

@@ -1,7 +1,9 @@
 """Build an experiment variant of libuflowcrc.so into abl/<name>.so: the product sources copied to a
 scratch tree, `file:old=>new` substitutions applied (each must match), compiled with the product's
 flags.  A/B measurement only (tools/ab_inproc.py); the product library is never touched.
-Usage: python tools/build_variant.py <name> 'frame_crc_varlen8.hip:old=>new' ..."""
+`file@path` replaces a source file of the copy with another file (e.g. an earlier round's, from git show);
+VARIANT_FLAGS (environment) adds hipcc flags.
+Usage: python tools/build_variant.py <name> 'frame_crc_varlen8.hip:old=>new' 'frame_parse.hip@/tmp/old.hip' ..."""
 import os
 import shutil
 import subprocess
@@ -20,6 +22,10 @@ def main():
     shutil.copytree(os.path.join(REPO, "uflow_amd", "csrc"), os.path.join(d, "uflow_amd", "csrc"))
     shutil.copytree(os.path.join(REPO, "include"), os.path.join(d, "include"))
     for sub in subs:
+        if "@" in sub and ":" not in sub.split("@", 1)[0]:
+            fn, src = sub.split("@", 1)
+            shutil.copy(src, os.path.join(d, "uflow_amd", "csrc", fn))
+            continue
         fn, rest = sub.split(":", 1)
         old, new = rest.split("=>", 1)
         p = os.path.join(d, "uflow_amd", "csrc", fn)
@@ -27,6 +33,7 @@ def main():
         assert old in s, f"{fn}: no match for {old!r}"
         open(p, "w").write(s.replace(old, new))
     sources, flags, _ = _build._native_identity()
+    flags = flags + os.environ.get("VARIANT_FLAGS", "").split()
     objs = []
     jobs = []
     for src in sources:

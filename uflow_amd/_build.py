@@ -65,8 +65,12 @@ def _native_identity(defines=()):
     deps += [os.path.join(REPO_DIR, "include", h) for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
     # No atomic optimizer: the lean kernel's single-lane claim atomics must stay plain
     # global_atomic_add (the optimizer reads the result back at once, forcing a vmcnt(0) wait).
+    # Uniform branches left unstructured: the variable-length kernel's set-level branches (a switch on
+    # the set's line count, masked or plain steps) otherwise get "Flow" blocks that copy the chain
+    # registers at every merge (1.585 against 1.484 ms on config 3, profiles/EXPERIMENTS.md).
     flags = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall",
-             "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
+             "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
+             "-mllvm", "-structurizecfg-skip-uniform-regions=true"]
     flags += ["-D" + d for d in defines]
     return sources, flags, _digest(deps + [os.path.abspath(__file__)], flags[1:])
 

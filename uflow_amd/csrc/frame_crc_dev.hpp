@@ -154,6 +154,12 @@ __host__ __device__ __forceinline__ uint32_t data_mask(int lb) {
   return lb >= 4 ? 0xFFFFFFFFu : (lb > 0 ? 0xFFFFFFFFu >> ((uint32_t)(32 - 8 * lb) & 31u) : 0u);
 }
 
+// The same from b = 8 lb (bits instead of bytes, any int): three VALU (clamp, 64-bit shift, not).
+__host__ __device__ __forceinline__ uint32_t data_mask_bits(int b) {
+  const uint32_t s = (uint32_t)(b < 0 ? 0 : (b > 32 ? 32 : b));
+  return ~(uint32_t)(0xFFFFFFFFFFFFFFFFull << s);
+}
+
 // Byte mask of the word whose first byte sits at frame offset ob, for a frame of len bytes: the
 // word's bytes at offsets [0, len).
 __host__ __device__ __forceinline__ uint32_t frame_word_mask(int ob, uint32_t len) {
@@ -171,7 +177,12 @@ __host__ __device__ __forceinline__ uint32_t frame_word_mask(int ob, uint32_t le
 __host__ __device__ __forceinline__ uint32_t rot_nibble_key(uint32_t col, uint32_t u, uint32_t e) {
   const uint32_t R = 31u - (e & 31u), sh = (8u * u) & 31u;
   const uint32_t steps = (0x03020100u >> sh) | (0x03020100u << ((32u - sh) & 31u));  // byte i = (i + u) & 3
-  return ((steps + (4u * (col & 7u) + R) * 0x01010101u) & 0x1F1F1F1Fu) << 2;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t rb = __builtin_amdgcn_perm(0u, R, 0u);  // R in every byte: one v_perm, not a 32-bit multiply
+#else
+  const uint32_t rb = R * 0x01010101u;
+#endif
+  return ((steps + (4u * (col & 7u)) * 0x01010101u + rb) & 0x1F1F1F1Fu) << 2;  // (the column part is per lane)
 }
 
 // Per-frame description for one 16-lane group.

@@ -3,31 +3,33 @@
 //
 // The batched CRC gate of Frame::read (src/frame/serial/mod.rs:675-690) and the frame seal
 // (serial/mod.rs:463-470, build.rs:151-159) for frame i = bytes[offsets[i] .. offsets[i+1]) (or
-// (start, end) pairs).  Same virtual stream as the other kernels (frame_crc_dev.hpp): the frame is
-// right-aligned into J 256-byte blocks behind zeros and G.  What differs is the lane layout:
-//   * A set is 8 frames, one per 8-lane group.  Lane col of a group loads two 16-byte pieces of
-//     each block, at 16 col and 128 + 16 col, so one wave-instruction still reads 128-byte runs and
-//     a set's frame loads whole 256-byte blocks.
-//   * The two pieces are consecutive 128-byte sub-blocks of one Horner chain per slot: 32 slots
-//     (lane col holds slots 4 col + b) with the constant A^128, i.e. V_s <- A^128 V_s ^ word twice
-//     per block.  The finish is lin = XOR_s A^(4(31-s)) V_s: 32 slot words per frame instead of
-//     64, so the per-frame finish (nibble lookups, the only per-frame LDS work) costs half.  On
-//     gfx950 every integer VALU instruction is 4 cycles per wave and the lean varlen kernels are
-//     VALU-bound (SQ_ACTIVE_INST_VALU ~ SQ_INSTS_VALU with the SIMD busy all along): per-frame work
-//     -- geometry, loads, front fix, finish, results -- is shared by 8 frames instead of 4.
-//   * Sets come from sorted runs: the wave that takes a run of 64 frames orders it by block count J
-//     (ballot ranks), so a set's 8 frames mostly share J (one uniform block loop, no frozen
-//     chains); a set mixing block counts freezes the chains of its shorter frames.
-//   * Windows end at the frame's end rounded up to 4 bytes, so every load is 4-byte aligned and
-//     needs no realignment: the t = 0..3 bytes past the frame are zeroed with the trailer, which
-//     multiplies the linear CRC by A^t, undone at the finish with one nibble-table product
-//     (A^-t, 8 lookups per frame instead of one v_perm per word and 4 DPP moves per block).
-//   * Loads are default-policy raw buffer loads from one resource per wave (the lines a frame
-//     shares with its neighbours, which sort into other sets, stay in L2 for them).  Lanes wholly
-//     before their frame and blocks past it load nothing (out-of-range offsets).
+// (start, end) pairs).  What this kernel does differently from the fixed-length one:
+//   * A set is 8 frames, one per 8-lane group; lane col of a group loads the 16 bytes at 16 col of
+//     each 128-byte line of its frame's window, so one wave-instruction reads 8 whole lines.
+//   * Windows are aligned to 128-byte lines: from the line holding G's first byte (4 bytes before the
+//     frame) to the line holding the frame's last byte, P lines.  Every load is one whole line, and
+//     the lines a frame shares with its neighbours are only its first and its last (default cache
+//     policy, so they stay in L2 for the neighbour, which the sort puts in another set); the lines in
+//     between are read once (non-temporal).  Measured as a loads-only pattern: 1.18 ms and 1.025 x the
+//     plain stream's requests on config 3, against 1.30 ms and 1.11 x for windows right-aligned to the
+//     frame's end (profiles/EXPERIMENTS.md, round 5).
+//   * Each lane's 4 words are 4 slot chains with the constant A^128 (32 slots per frame); the stream
+//     ends at the word holding the frame's last byte (slot e, t = 0..3 bytes past the frame), so the
+//     finish takes the slot constants rotated by e (group_lin8_rot) and undoes A^t with one nibble-table
+//     product.  Words past a frame's end step nothing; the bytes past its data are masked out.
+//   * Slots run right-aligned: position s = 0 .. 12 holds line s - 13 + P, so every frame's last line
+//     is at position 12 and the lines before a frame's first are zeros (chains stay zero).  A set runs
+//     positions 13 - Pmax .. 12 straight through, entered by one switch on its longest frame; line 0
+//     (slot 0, loaded apart for its cache policy) goes in at position 13 - P.  Only positions 11 and
+//     12 can need masked steps.
+//   * Sets come from runs of 64 frames sorted by line count in the wave that takes them (four one-bit
+//     radix split passes); the per-set facts come once per run from half-row reductions and ballots.
 //   * Results of a run (8 sets x 8 frames) collect in one register pair per lane and leave with
 //     hidden stores once per run.  Sets with a frame the fast path cannot take (shorter than 4 B,
-//     longer than 6 blocks, at the batch edges, past its end) run byte-wise, in the same loop.
+//     longer than 13 lines, at the batch edges, past its end) run byte-wise, in the same loop (the
+//     byte path keeps the 256-byte block layout of frame_crc_dev.hpp: block8 below).
+//   * Built with uniform branches left unstructured (_build.py): the set-level branches otherwise get
+//     register-copy blocks at every merge.
 #include <type_traits>
 
 #include "frame_crc_dev.hpp"
@@ -37,7 +39,7 @@ namespace ufc_dev {
 namespace {
 
 constexpr int kV8Pieces = 13;              // fast path: windows of up to 13 lines (frames of 4..1532 B)
-constexpr int kV8Split = 7;                // slots 0 .. 6 in a set's first load part, 7 .. 12 and 1 in its second
+constexpr int kV8Split = 7;                // slots 0 .. 6 in a set's first load part, 7 .. 12 in its second
 constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the run's base - bias
 constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
@@ -50,13 +52,17 @@ constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
 // Per-lane geometry of a frame on the fast path (one VGPR): r = (frame start - 4) mod 128 [0,7) (the
 // window starts at the 128-byte line holding G's first byte, r bytes before it), len [7,18), index
 // in its run [18,24); then the set's facts, the same in every lane of the set: Pmax = its frames' most
-// lines, 0 for a byte-path set [24,28), plim = lines 0 .. plim-1 hold CRC'd data only in every frame
-// [28,32).  The trailer's first byte lies at window offset zo = len + r; lines P = ceil((zo + 4) / 128).
+// lines, 0 for a byte-path set [24,28), Pmin = their fewest [28,32).  The trailer's first byte lies at
+// window offset zo = len + r; lines P = ceil((zo + 4) / 128).  The window start's word (wrel) keeps
+// bits 7.. of the start in [0,24) (its low 7 bits are the same for the whole run) and two more set
+// facts: kV8PenultData (no frame's trailer starts in its line P - 2: that line holds CRC'd data only
+// wherever it is a frame's) and kV8G1 (a frame's G reaches into line 1: r >= 125).
 __device__ __forceinline__ uint32_t w_r(uint32_t g) { return g & 127u; }
 __device__ __forceinline__ uint32_t w_len(uint32_t g) { return (g >> 7) & 2047u; }
 __device__ __forceinline__ uint32_t w_zo(uint32_t g) { return w_len(g) + w_r(g); }
 __device__ __forceinline__ uint32_t w_P(uint32_t g) { return (w_zo(g) + 131u) >> 7; }
 __device__ __forceinline__ uint32_t w_orig(uint32_t g) { return (g >> 18) & 63u; }
+constexpr uint32_t kV8PenultData = 1u << 25, kV8G1 = 1u << 26;
 
 struct Lane8 {
   const char* lds;
@@ -147,10 +153,11 @@ __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
 // the CRC'd data.  Words before the frame's end (the data's and the trailer's) step their slots,
 // the trailer's bytes and those past the data as zeros; words past the frame's end do not step.
 __device__ __forceinline__ void chain4_masked(const Lane8& L, Chains& c, uint4 x, int lim) {
-  const uint32_t n0 = chain_step(L.lds, c.v0, L.K, x.x & data_mask(lim));
-  const uint32_t n1 = chain_step(L.lds, c.v1, L.K, x.y & data_mask(lim - 4));
-  const uint32_t n2 = chain_step(L.lds, c.v2, L.K, x.z & data_mask(lim - 8));
-  const uint32_t n3 = chain_step(L.lds, c.v3, L.K, x.w & data_mask(lim - 12));
+  const int b = 8 * lim;
+  const uint32_t n0 = chain_step(L.lds, c.v0, L.K, x.x & data_mask_bits(b));
+  const uint32_t n1 = chain_step(L.lds, c.v1, L.K, x.y & data_mask_bits(b - 32));
+  const uint32_t n2 = chain_step(L.lds, c.v2, L.K, x.z & data_mask_bits(b - 64));
+  const uint32_t n3 = chain_step(L.lds, c.v3, L.K, x.w & data_mask_bits(b - 96));
   c.v0 = lim > -4 ? n0 : c.v0;
   c.v1 = lim > 0 ? n1 : c.v1;
   c.v2 = lim > 4 ? n2 : c.v2;
@@ -200,13 +207,16 @@ __device__ __forceinline__ void block8(const Lane8& L, uint32_t j, uint32_t J, u
 }
 
 struct Set8Meta {
-  uint32_t Pmax;  // most lines of the set's frames
-  uint32_t plim;  // lines 0 .. plim-1 hold CRC'd data only, in every frame of the set
-  bool slow;      // byte path
+  uint32_t Pmax;    // most lines of the set's frames
+  uint32_t Pmin;    // fewest
+  bool penult_data;  // no frame's trailer starts in its line P - 2
+  bool g1;          // a frame's G reaches into its line 1
+  bool slow;        // byte path
 };
 
-// A set's loads: slot 0 = line 0, slot 1 = the frame's last line, slot k >= 2 = line k - 1; tr =
-// the trailer (4 bytes at zo).
+// A set's loads, right-aligned: slot 0 = line 0, slot s >= 1 = line s - 13 + P (its last line P - 1 in
+// slot 12; slots that would hold line 0 or a line before it are out of range, zeros); tr = the
+// trailer (4 bytes at zo).
 struct Buf13 {
   uint4 x[kV8Pieces];
   uint32_t tr = 0;
@@ -303,37 +313,44 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     const uint64_t sb = run_base(a);
     const FGeo fg = frame_geo(a, len, live, sb);
     const uint32_t key = !live ? 15u : (fg.bad ? 14u : w_P(fg.geo));  // (a set with a dead frame: byte path)
-    uint32_t below = 0, rank_in = 0;
+    // Stable counting order by key: four one-bit split passes (LSD radix) over (key, lane) words,
+    // each moved to its new position with one ds_permute; then sorted position i holds frame src.
+    uint32_t v = (key << 6) | L.lane;
 #pragma unroll
-    for (uint32_t k = 1; k <= 15; k++) {
-      const uint64_t m = __builtin_amdgcn_ballot_w64(key == k);
-      below += (k < key) ? (uint32_t)__builtin_popcountll(m) : 0u;
-      const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-      rank_in = (k == key) ? rk : rank_in;
+    for (uint32_t b = 6; b < 10; b++) {
+      const bool one = ((v >> b) & 1u) != 0;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(one);
+      const uint32_t ob = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      const uint32_t pos = one ? 64u - (uint32_t)__builtin_popcountll(m) + ob : L.lane - ob;
+      v = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos * 4u), (int)v);
     }
-    const int dst = (int)((below + rank_in) * 4u);
+    const int src = (int)((v & 63u) * 4u);
     if (!raw) {
       // lane = sorted position: per-set facts over each 8-lane half-row, into geo bits 24..31
-      const uint32_t geo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.geo);
-      const uint32_t bad = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(key >= 14u ? 1u : 0u));
-      out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)fg.wrel);
+      const uint32_t geo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)fg.geo);
+      const uint32_t bad = (v >> 6) >= 14u ? 1u : 0u;
+      out.a_hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)fg.wrel);
       out.sb = sb;
-      uint32_t px = w_P(geo), zn = w_zo(geo) >> 7;
+      const uint32_t P = w_P(geo), zo = w_zo(geo);
+      uint32_t px = P, pn = P;
       px = max(px, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)px, 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
-      zn = min(zn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)zn, 0xB1, 0xF, 0xF, false));
+      pn = min(pn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pn, 0xB1, 0xF, 0xF, false));
       px = max(px, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)px, 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
-      zn = min(zn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)zn, 0x4E, 0xF, 0xF, false));
+      pn = min(pn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pn, 0x4E, 0xF, 0xF, false));
       px = max(px, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)px, 0x141, 0xF, 0xF, false));  // row_half_mirror
-      zn = min(zn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)zn, 0x141, 0xF, 0xF, false));
-      const uint64_t mbad = __builtin_amdgcn_ballot_w64(bad != 0u);
-      const bool slow = ((mbad >> (L.lane & ~7u)) & 0xFFu) != 0;
-      out.a_lo = (geo & 0xFFFFFFu) | ((slow ? 0u : min(px, 15u)) << 24) | (min(zn, 15u) << 28);
+      pn = min(pn, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pn, 0x141, 0xF, 0xF, false));
+      const uint32_t hr = L.lane & ~7u;  // the set's half-row
+      const bool slow = ((__builtin_amdgcn_ballot_w64(bad != 0u) >> hr) & 0xFFu) != 0;
+      const bool pe = ((__builtin_amdgcn_ballot_w64(P >= 2u && zo < 128u * (P - 1u)) >> hr) & 0xFFu) == 0;
+      const bool g1 = ((__builtin_amdgcn_ballot_w64(w_r(geo) >= 125u) >> hr) & 0xFFu) != 0;
+      out.a_lo = (geo & 0xFFFFFFu) | ((slow ? 0u : min(px, 15u)) << 24) | (min(pn, 15u) << 28);
+      out.a_hi = (out.a_hi >> 7) | (pe ? kV8PenultData : 0u) | (g1 ? kV8G1 : 0u);
       return;
     }
-    out.a_lo = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)a);
-    out.a_hi = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)(a >> 32));
-    out.len = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(uint32_t)min(len, (uint64_t)0xFFFFFFFFu));
-    out.info = (uint32_t)__builtin_amdgcn_ds_permute(dst, (int)(L.lane | (live ? 0u : 0x80000000u)));
+    out.a_lo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)a);
+    out.a_hi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(a >> 32));
+    out.len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)min(len, (uint64_t)0xFFFFFFFFu));
+    out.info = (v & 63u) | ((v >> 6) == 15u ? 0x80000000u : 0u);
   };
   // The raw words of this group's frame of set q (the same in the group's 8 lanes): start lo, hi,
   // length, index | dead.
@@ -392,33 +409,44 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   auto geometry = [&](uint32_t q, const Rec& r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
     sb = r.sb;
     const uint32_t gu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.geo);
+    const uint32_t hu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.wrel);
     m.Pmax = (gu >> 24) & 15u;
-    m.plim = gu >> 28;
+    m.Pmin = gu >> 28;
+    m.penult_data = (hu & kV8PenultData) != 0;
+    m.g1 = (hu & kV8G1) != 0;
     m.slow = m.Pmax == 0u;
     const bool live = q != kNoSet && !m.slow;
-    voff0 = live ? r.wrel + 16u * L.col : kV8Oob;
+    // (the window start's low 7 bits: bytes + sb + start is 128-byte aligned)
+    const uint32_t low7 = (0u - (uint32_t)(uintptr_t)p.bytes - (uint32_t)sb) & 127u;
+    voff0 = live ? (((r.wrel & 0xFFFFFFu) << 7) | low7) + 16u * L.col : kV8Oob;
     return r.geo;
   };
-  // The set's loads (struct Buf13): slots 0 and 1, the lines the frame shares with its neighbours
-  // (which the sort puts in other sets), with default policy so that they stay in L2 for them; the
-  // lines in between, each read by this set alone, non-temporal; lanes wholly before G, lines past the
-  // frame's own and a frame's second slot when it has one line are out of range (zeros, no request).
-  // Then the trailer, one dword at zo.
-  // Issued in two parts (PART 0: slots 0 and 2 .. kV8Split - 1 and the trailer; PART 1: the rest), the
-  // second in the middle of the previous set's compute, once its first lines' registers are free.
+  // The set's loads (struct Buf13): line 0 (slot 0) and the last line (slot 12), the lines the frame
+  // shares with its neighbours (which the sort puts in other sets), with default policy so that they
+  // stay in L2 for them; the lines in between, each read by this set alone, non-temporal; lanes wholly
+  // before G and slots before a frame's line 1 are out of range (zeros, no request).  Then the trailer,
+  // one dword at zo.  Issued in two parts (PART 0: slots 0 .. kV8Split - 1 and the trailer; PART 1:
+  // the rest), the second during the previous set's compute, once its early slots' registers are free.
   auto load_set = [&](uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b, auto part) {
     constexpr int PART = decltype(part)::value;
     const uint32_t P = w_P(geo), front = w_r(geo) + 4u;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
+    // slot s at base + 128 s (line s - 13 + P); (an out-of-range voff0 keeps base out of range for every
+    // slot it is used in: s + P >= 14; the run base's bias keeps base itself above 0)
+    const uint32_t base = voff0 + 128u * P - 128u * 13u;
     if constexpr (PART == 0) {
       const uint32_t vo = (16u * L.col + 16u <= front) ? kV8Oob : voff0;
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8AuxShared);
       b.x[0] = make_uint4(v.x, v.y, v.z, v.w);
     }
 #pragma unroll
-    for (int k = PART == 0 ? 2 : kV8Split; k < (PART == 0 ? kV8Split : kV8Pieces); k++) {  // line k - 1
-      const uint32_t vo = (uint32_t)k + 1u <= P ? voff0 : kV8Oob;  // (an out-of-range base stays out of range)
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)(k - 1)), 0, kV8AuxInterior);
+    for (int k = PART == 0 ? 1 : kV8Split; k < (PART == 0 ? kV8Split : kV8Pieces); k++) {
+      const uint32_t vo = (uint32_t)k + P >= 14u ? base : kV8Oob;
+      u32x4 v;
+      if (k == kV8Pieces - 1)
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxShared);
+      else
+        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxInterior);
       b.x[k] = make_uint4(v.x, v.y, v.z, v.w);
     }
     if constexpr (PART == 0) {
@@ -426,10 +454,6 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
         const uint32_t vt = voff0 == kV8Oob ? kV8Oob : voff0 - 16u * L.col + w_zo(geo);
         b.tr = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vt, 0, kV8AuxShared);
       }
-    } else {
-      const uint32_t vo = P >= 2u ? voff0 + 128u * (P - 1u) : kV8Oob;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8AuxShared);
-      b.x[1] = make_uint4(v.x, v.y, v.z, v.w);
     }
   };
   using Part0 = std::integral_constant<int, 0>;
@@ -460,45 +484,90 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // Fast set.  The stream of a frame is its window with the bytes before G zeroed, G, the data, the
   // trailer as zeros, up to the end of the word holding the frame's last byte (e: that word's slot,
   // t = 0..3 bytes past the frame in it): lin = A^t (register after the data), undone at the finish.
-  // Line order: slot 0 (line 0), slots 2.. (lines 1 .. P-2), slot 1 (line P-1); lines past a frame's
-  // own step nothing (masked), so every frame's slots see its lines in order.
+  // The slots run right-aligned: position s = 0 .. 12 holds line s - 13 + P of each frame, so every
+  // frame's last line is at position 12 and its line 0 at 13 - P (line 0 comes from slot 0: it is put
+  // in at that position, front-fixed).  Positions before a frame's line 0 hold zeros, which leave its
+  // chains at zero: the set runs positions 13 - Pmax .. 12 straight through, every lane stepping at
+  // every position, entered once by a switch on Pmax (one merge of the chain registers per set).  Only
+  // positions 11 and 12 (lines P - 2 and P - 1) can hold bytes past the CRC'd data (masked steps).
   auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf13& b, uint32_t voff0, uint64_t sb, auto mid) {
+    static_assert(kV8Split == 7 && kV8Pieces == 13, "the position sequence below");
     const uint32_t zo = w_zo(geo), P = w_P(geo), front = w_r(geo) + 4u;
     const int lim0 = (int)zo - (int)(16u * L.col);
+    const int lim12 = lim0 - 128 * (int)(P - 1u), lim11 = lim12 + 128;
+    const int g1 = 128 + (int)(16u * L.col) - (int)front;  // G's last bytes in line 1 (r >= 125)
+    const uint4 fx = fix_piece(L.lds, b.x[0], (int)front - (int)(16u * L.col));  // line 0
+    const uint32_t Iend = 13u - m.Pmin;  // positions holding some frame's line 0: 13 - Pmax .. Iend
+    auto xin = [&](int s) -> uint4 {  // position s's piece
+      uint4 x = s == 0 ? make_uint4(0u, 0u, 0u, 0u) : b.x[s];
+      if ((uint32_t)s <= Iend) {
+        const bool l0 = (uint32_t)s + P == 13u;
+        x = make_uint4(l0 ? fx.x : x.x, l0 ? fx.y : x.y, l0 ? fx.z : x.z, l0 ? fx.w : x.w);
+      }
+      if (m.g1 && (uint32_t)s + m.Pmax >= 14u && (uint32_t)s <= Iend + 1u)
+        x.x = fix_word(x.x, (uint32_t)s + P == 14u ? g1 : 0, L.G);
+      return x;
+    };
     Chains c{0u, 0u, 0u, 0u, 0u};
-    {  // line 0: zeros before G, G, the frame's first bytes
-      const uint4 x = fix_piece(L.lds, b.x[0], (int)front - (int)(16u * L.col));
-      if (m.plim >= 1u) {
-        c.v0 = x.x;
-        c.v1 = x.y;
-        c.v2 = x.z;
-        c.v3 = x.w;
-      } else {
-        c.v0 = x.x & data_mask(lim0);
-        c.v1 = x.y & data_mask(lim0 - 4);
-        c.v2 = x.z & data_mask(lim0 - 8);
-        c.v3 = x.w & data_mask(lim0 - 12);
-      }
-    }
-#pragma unroll
-    for (int j = 1; j < kV8Pieces - 1; j++) {  // line j from slot j + 1
-      if (j + 1 == kV8Split) {  // slots 2 .. kV8Split - 1 consumed: the next set's second part
-        __builtin_amdgcn_sched_barrier(0);
-        mid();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      uint4 x = b.x[j + 1];
-      if (j == 1) x.x = fix_word(x.x, 128 + (int)(16u * L.col) - (int)front, L.G);  // G's last bytes (r >= 125)
-      if ((uint32_t)j < m.plim)
+    auto masked_init = [&](uint4 x, int lim) {  // from zero chains: words past the end stay zero
+      const int bb = 8 * lim;
+      c.v0 = x.x & data_mask_bits(bb);
+      c.v1 = x.y & data_mask_bits(bb - 32);
+      c.v2 = x.z & data_mask_bits(bb - 64);
+      c.v3 = x.w & data_mask_bits(bb - 96);
+    };
+    auto entry = [&](int s) {
+      const uint4 x = xin(s);
+      if (s == 12)
+        masked_init(x, lim12);
+      else if (s == 11 && !m.penult_data)
+        masked_init(x, lim11);
+      else
+        c = Chains{x.x, x.y, x.z, x.w, 0u};
+    };
+    auto stepk = [&](int s) {
+      const uint4 x = xin(s);
+      if (s == 12)
+        chain4_masked(L, c, x, lim12);
+      else if (s == 11 && !m.penult_data)
+        chain4_masked(L, c, x, lim11);
+      else
         chain4(L, c, x);
-      else if ((uint32_t)j + 1u < m.Pmax)
-        chain4_masked(L, c, x, (uint32_t)j + 1u < P ? lim0 - 128 * j : -4);
+    };
+    auto midk = [&]() {  // the next set's second part: slots 1 .. kV8Split - 1 of this one are done
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    switch (m.Pmax) {  // enter at position 13 - Pmax
+      case 13: entry(0); goto p1;
+      case 12: entry(1); goto p2;
+      case 11: entry(2); goto p3;
+      case 10: entry(3); goto p4;
+      case 9: entry(4); goto p5;
+      case 8: entry(5); goto p6;
+      case 7: entry(6); goto p7;
+      case 6: entry(7); midk(); goto p8;
+      case 5: entry(8); midk(); goto p9;
+      case 4: entry(9); midk(); goto p10;
+      case 3: entry(10); midk(); goto p11;
+      case 2: entry(11); midk(); goto p12;
+      default: entry(12); midk(); goto p13;
     }
-    if (m.Pmax >= 2u) {  // the last line (a one-line frame: no step)
-      uint4 x = b.x[1];
-      if (P == 2u) x.x = fix_word(x.x, 128 + (int)(16u * L.col) - (int)front, L.G);
-      chain4_masked(L, c, x, P >= 2u ? lim0 - 128 * (int)(P - 1u) : -4);
-    }
+  p1: stepk(1);
+  p2: stepk(2);
+  p3: stepk(3);
+  p4: stepk(4);
+  p5: stepk(5);
+  p6: stepk(6);
+  p7: midk();
+    stepk(7);
+  p8: stepk(8);
+  p9: stepk(9);
+  p10: stepk(10);
+  p11: stepk(11);
+  p12: stepk(12);
+  p13:
     const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
     const uint32_t crc = ~unshift(group_lin8_rot(L, c, e), t);
     const uint32_t ok = (!SEAL && w_len(geo) >= 5u && __builtin_bswap32(b.tr) == crc) ? 1u : 0u;

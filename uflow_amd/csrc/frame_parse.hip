@@ -42,7 +42,6 @@ constexpr uint32_t kPosSlots = UFC_POS_SLOTS;  // datagram headers recorded per 
 constexpr uint64_t kSegWords = (uint64_t)kPosSlots * kParseThreads;  // u16 per workgroup segment
 enum : uint8_t { kItemsNone = 0, kItemsPos = 1, kItemsAck = 2, kItemsWalk = 3 };
 
-typedef hipcub::BlockScan<uint32_t, kParseThreads> BlockScan;
 // Two per-frame counts scanned at once (each workgroup sum < 2^32: 256 frames x < 2^24), low and high halves.
 typedef hipcub::BlockScan<uint64_t, kParseThreads> BlockScan2;
 
@@ -64,12 +63,12 @@ struct DevBytes {
   }
 };
 
-// The walk's reader: the frame's first 16 bytes (kind, the data header's fields and the first
-// datagram's size bytes; every field of an ack frame's header) come from one 16-byte load issued with
-// the frame's other first reads when the frame has 16 bytes, bytes 0..7 from one 8-byte load when it
-// has 8 to 15; the rest as DevBytes.  held_byte keeps every shift amount in range: an out-of-range
-// shift in the unselected arm of a ternary let the compiler treat a byte as undefined (data frames
-// failing at random, profiles/EXPERIMENTS.md).
+// The walk's reader: the frame's first HEAD bytes come from one load issued with the frame's other
+// first reads (HEAD = 16: kind, the data header's fields and the first datagram's size bytes, every
+// field of an ack frame's header; HEAD = 8: bytes 0..7), the rest as DevBytes.  The product walk uses
+// HEAD = 8: round 4's 16-byte head failed at random (one data frame per ~200k, a different one each
+// run) and its cause is not shown (profiles/EXPERIMENTS.md), so it stays out (it bought
+// ~2 %: 0.419 against 0.4105 ms).  head_byte keeps every shift amount in range.
 typedef unsigned int u32x4_h __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1), aligned(1))) u32x4_h g_u32x4_h;
 template <uint32_t HEAD = 16>
@@ -100,15 +99,6 @@ struct DevBytesHead {
     if (i + 3 <= held) return held_byte(i) | (held_byte(i + 1) << 8) | (held_byte(i + 2) << 16);
     return *(g_u32_a1*)(p + i) & 0xFFFFFFu;
   }
-};
-
-// Walk sink: only the header offsets, into this thread's LDS slots (slot k at k * kParseThreads).
-struct PosSink {
-  static constexpr bool kDecode = false;
-  uint16_t* slot;
-  __device__ bool on() const { return true; }
-  __device__ void operator()(uint32_t, const ufc_item&) const {}
-  __device__ void header(uint32_t k, uint32_t off) const { slot[k * kParseThreads] = (uint16_t)off; }
 };
 
 // Items as three 8-byte stores each (ufc_item is 24 bytes, laid out as below).
@@ -150,65 +140,6 @@ __device__ __forceinline__ uint32_t frame_len32(const uint64_t* offsets, uint64_
   const uint64_t b = offsets[i + 1];
   const uint64_t len64 = b >= a ? b - a : 0;
   return len64 > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)len64;
-}
-
-__global__ __launch_bounds__(kParseThreads) void parse_walk_kernel(const uint8_t* bytes, const uint64_t* offsets,
-                                                                   uint64_t n, const uint8_t* valid,
-                                                                   ufc_frame_info* infos, uint32_t* counts,
-                                                                   uint8_t* modes, uint16_t* pos_seg,
-                                                                   unsigned long long* seg_cursor, uint32_t* seg_base,
-                                                                   uint64_t seg_cap, uint32_t* wg_counts) {
-  __shared__ uint16_t slots[kSegWords];
-  __shared__ typename BlockScan2::TempStorage scan_tmp;
-  __shared__ uint32_t base_lds;
-  const uint32_t t = threadIdx.x;
-  const uint64_t i = (uint64_t)blockIdx.x * kParseThreads + t;
-  uint32_t npos = 0;
-  uint8_t mode = kItemsNone;
-  uint32_t cnt_all = 0;
-  if (i < n) {
-    uint64_t a;
-    const uint32_t len = frame_len32(offsets, i, a);
-    ufc_frame_info info;
-    const bool ok = ufc_codec::read_frame_to(DevBytes{bytes + a}, len, valid[i] != 0, info, PosSink{slots + t},
-                                             kPosSlots);
-    const uint32_t cnt = ok ? info.item_count : 0u;
-    if (cnt) {
-      if (info.kind == UFC_FRAME_ACK) {
-        mode = kItemsAck;
-      } else if (cnt <= kPosSlots && len <= 0xFFFFu) {
-        mode = kItemsPos;
-        npos = cnt;
-      } else {
-        mode = kItemsWalk;
-      }
-    }
-    info.item_first = 0;  // written by the emit step
-    infos[i] = info;
-    counts[i] = cnt;
-    cnt_all = cnt;
-  }
-  // header slots (low half) and items (high half) of the workgroup's frames, one scan
-  uint64_t lo2, total2;
-  BlockScan2(scan_tmp).ExclusiveSum((uint64_t)npos | ((uint64_t)cnt_all << 32), lo2, total2);
-  const uint32_t lo = (uint32_t)lo2, total = (uint32_t)total2;
-  if (t == 0) wg_counts[blockIdx.x] = (uint32_t)(total2 >> 32);  // (scanned over the workgroups next)
-  // the workgroup's segment of header slots, from the launch's bump counter (no room: the emit
-  // step re-walks this workgroup's frames instead)
-  if (t == 0) {
-    // (64-bit cursor: the sum of every workgroup's total may pass 2^32 long after the cap is reached)
-    const unsigned long long b64 = total ? atomicAdd(seg_cursor, (unsigned long long)total) : 0ull;
-    const uint32_t b = (total && b64 + total > seg_cap) ? 0xFFFFFFFFu : (uint32_t)b64;
-    base_lds = b;
-    seg_base[blockIdx.x] = b;
-  }
-  __syncthreads();
-  const uint32_t base = base_lds;
-  if (i < n) modes[i] = (mode == kItemsPos && base == 0xFFFFFFFFu) ? (uint8_t)kItemsWalk : mode;
-  if (base != 0xFFFFFFFFu) {  // (each thread reads back only the slots it wrote)
-    uint16_t* seg = pos_seg + base;
-    for (uint32_t k = 0; k < npos; k++) seg[lo + k] = slots[k * kParseThreads + t];
-  }
 }
 
 // The walk with pooled header slots (round 3): kInlineSlots slots per frame in LDS, and the headers
@@ -273,7 +204,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
-    const DevBytesHead<16> rd = DevBytesHead<16>::load(bytes + a, len);
+    const DevBytesHead<8> rd = DevBytesHead<8>::load(bytes + a, len);
     const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
     const uint32_t cnt = ok ? info.item_count : 0u;
@@ -475,204 +406,6 @@ __global__ __launch_bounds__(kParseThreads) void parse_emit_kernel(
   }
 }
 
-// ---- One-pass parse (round 5): walk, item scan and emit in one kernel ----
-// Each workgroup takes the next tile of 256 frames from a launch counter (so tiles start in order),
-// walks them (one thread per frame, header offsets in LDS: 16 inline slots per frame, then 16-slot
-// chunks of a workgroup pool, at most 7 per frame), scans its item counts, learns its first item from
-// its predecessors by decoupled look-back (one 8-byte word per tile: flag | count, agent-scope relaxed
-// atomic stores and polls, MI355X_MICROARCH.md's granule hand-off), writes each frame's info once
-// with its item_first, and emits its items at once: item-parallel, each header read again while the
-// lines the walk just read are still in the caches -- no header slots through memory, no scan launch,
-// no second pass over the batch from HBM.  The walk reads each frame's first 8 bytes in one load
-// (the 16-byte head stays out until the cause of its round-4 failures is shown).
-constexpr uint32_t kFusedInline = 16;
-constexpr uint32_t kFusedChunk = 16;
-constexpr uint32_t kFusedPoolChunks = 128;
-constexpr uint32_t kFusedMaxChunks = 7;  // 16 + 7 * 16 = 128 > the 127 datagrams of a data frame
-constexpr uint64_t kLbAggregate = 1ull << 62, kLbPrefix = 1ull << 63, kLbValue = kLbAggregate - 1;
-
-struct ChunkSink {
-  static constexpr bool kDecode = false;
-  uint16_t* inl;      // this thread's inline slots (slot k at k * kParseThreads)
-  uint16_t* pool;     // the workgroup's pool of chunks
-  uint32_t* pctr;     // its chunk counter
-  uint8_t* cids;      // this thread's chunk ids (chunk c at c * kParseThreads)
-  bool* full;
-  __device__ bool on() const { return true; }
-  __device__ void operator()(uint32_t, const ufc_item&) const {}
-  __device__ void header(uint32_t k, uint32_t off) const {
-    if (k < kFusedInline) {
-      inl[k * kParseThreads] = (uint16_t)off;
-      return;
-    }
-    if (*full) return;
-    const uint32_t kk = k - kFusedInline, c = kk / kFusedChunk;
-    if (kk % kFusedChunk == 0) {
-      const uint32_t id = c < kFusedMaxChunks ? atomicAdd(pctr, 1u) : kFusedPoolChunks;  // (LDS atomic)
-      if (id >= kFusedPoolChunks) {
-        *full = true;
-        return;
-      }
-      cids[c * kParseThreads] = (uint8_t)id;
-    }
-    pool[cids[c * kParseThreads] * kFusedChunk + kk % kFusedChunk] = (uint16_t)off;
-  }
-};
-
-__global__ __launch_bounds__(kParseThreads) void parse_fused_kernel(const uint8_t* bytes, const uint64_t* offsets,
-                                                                    uint64_t n, const uint8_t* valid,
-                                                                    ufc_frame_info* infos, ufc_item* items,
-                                                                    uint64_t cap, uint64_t* items_used,
-                                                                    uint32_t* tile_ctr, uint64_t* lb) {
-  __shared__ uint16_t inl[kFusedInline * kParseThreads];
-  __shared__ uint16_t pool[kFusedPoolChunks * kFusedChunk];
-  __shared__ uint8_t cids[kFusedMaxChunks * kParseThreads];
-  __shared__ uint32_t lfirst[kParseThreads];
-  __shared__ uint64_t lstart[kParseThreads];
-  __shared__ uint8_t lmode[kParseThreads];
-  __shared__ typename BlockScan::TempStorage scan_tmp;
-  __shared__ uint32_t s_tile, s_pctr, s_end;
-  __shared__ uint64_t s_base;
-  const uint32_t t = threadIdx.x;
-  if (t == 0) {
-    s_tile = atomicAdd(tile_ctr, 1u);  // tiles start in claim order: every lower tile has started
-    s_pctr = 0;
-  }
-  __syncthreads();
-  const uint64_t tile = s_tile;
-  const uint64_t i0 = tile * kParseThreads, i = i0 + t;
-  const uint32_t nb = (uint32_t)min((uint64_t)kParseThreads, n - i0);  // frames of this tile
-  uint32_t cnt = 0;
-  uint8_t mode = kItemsNone;
-  uint64_t a = 0;
-  bool full = false;
-  ufc_frame_info info{};
-  if (i < n) {
-    const uint32_t len = frame_len32(offsets, i, a);
-    const DevBytesHead<8> rd = DevBytesHead<8>::load(bytes + a, len);
-    const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
-                                             ChunkSink{inl + t, pool, &s_pctr, cids + t, &full}, kPosSlots * 2);
-    cnt = ok ? info.item_count : 0u;
-    if (cnt) {
-      if (info.kind == UFC_FRAME_ACK)
-        mode = kItemsAck;
-      else if (!full && len <= 0xFFFFu)
-        mode = kItemsPos;
-      else
-        mode = kItemsWalk;
-    }
-  }
-  uint32_t lo, total;
-  BlockScan(scan_tmp).ExclusiveSum(cnt, lo, total);
-  if (t == 0) {  // decoupled look-back over the tiles before this one
-    uint64_t base = 0;
-    if (tile == 0) {
-      __hip_atomic_store(lb, kLbPrefix | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(lb + tile, kLbAggregate | (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      for (uint64_t q = tile - 1;;) {
-        const uint64_t v = __hip_atomic_load(lb + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((v & (kLbAggregate | kLbPrefix)) == 0) {
-          __builtin_amdgcn_s_sleep(2);
-          continue;
-        }
-        base += v & kLbValue;
-        if ((v & kLbPrefix) || q == 0) break;
-        q--;
-      }
-      __hip_atomic_store(lb + tile, kLbPrefix | (base + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_base = base;
-    s_end = total;
-  }
-  __syncthreads();
-  const uint64_t wbase = s_base;
-  const uint64_t first = wbase + lo;
-  if (i < n) {
-    info.item_first = (uint32_t)first;
-    infos[i] = info;
-    if (i == n - 1 && items_used) *items_used = first + cnt;
-  }
-  lfirst[t] = lo;
-  lstart[t] = a;
-  lmode[t] = mode;
-  __syncthreads();
-  if (!items) return;
-
-  // Header bytes through a buffer resource over the tile's bytes (as parse_emit_kernel).
-  const uint64_t span_lo = lstart[0];
-  const uint64_t span_hi = offsets[i0 + nb];
-  const uintptr_t base_addr = (uintptr_t)(bytes + span_lo);
-  const uint32_t delta = (uint32_t)(base_addr & 3u);
-  const uint64_t range = (span_hi - span_lo + delta + 3) & ~(uint64_t)3;
-  const bool buf_ok = span_hi >= span_lo && range < 0xFFFFFFF0ull;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(base_addr - delta), 0, buf_ok ? (int)(uint32_t)range : 0, 0x00020000);
-  const uint32_t g_end = (uint32_t)min((uint64_t)s_end, cap > wbase ? cap - wbase : 0ull);
-  for (uint32_t g = t; g < g_end; g += kParseThreads) {
-    uint32_t lo_f = 0, hi_f = nb - 1;  // owner: the last frame whose first item is <= g
-    while (lo_f < hi_f) {
-      const uint32_t mid = (lo_f + hi_f + 1) >> 1;
-      if (lfirst[mid] <= g)
-        lo_f = mid;
-      else
-        hi_f = mid - 1;
-    }
-    const uint32_t f = lo_f, k = g - lfirst[f];
-    const uint8_t m = lmode[f];
-    if (m != kItemsPos && m != kItemsAck) continue;  // (kItemsWalk: the frame's own thread, below)
-    uint32_t hoff;
-    if (m == kItemsAck) {
-      hoff = 1u + ufc_codec::kAckPayloadHeader + UFC_ACK_GROUP_SIZE * k;
-    } else if (k < kFusedInline) {
-      hoff = inl[k * kParseThreads + f];
-    } else {
-      const uint32_t kk = k - kFusedInline;
-      hoff = pool[cids[(kk / kFusedChunk) * kParseThreads + f] * kFusedChunk + kk % kFusedChunk];
-    }
-    uint32_t w[4];
-    if (buf_ok) {
-      const uint32_t ex = (uint32_t)(lstart[f] - span_lo) + delta + hoff;
-      if (ex + 16 <= (uint32_t)range) {  // one unaligned 16-byte load at the header
-        const u32x4_h v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)ex, 0, 0);
-        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-      } else {  // (a header at the very end of the span: an aligned 16-byte + 4-byte pair)
-        const uint32_t al = ex & ~3u, sh = ex & 3u;
-        const u32x4_h v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)al, 0, 0);
-        const uint32_t x4 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(al + 16), 0, 0);
-        w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, sh);
-        w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, sh);
-        w[2] = __builtin_amdgcn_alignbyte(v.w, v.z, sh);
-        w[3] = __builtin_amdgcn_alignbyte(x4, v.w, sh);
-      }
-    } else {
-      const DevBytes rd{bytes + lstart[f] + hoff};
-      for (int q = 0; q < 4; q++) w[q] = 0;
-      const uint32_t nbytes = m == kItemsAck ? UFC_ACK_GROUP_SIZE : 14u;
-      for (uint32_t c = 0; c < nbytes; c++) w[c >> 2] |= rd(c) << (8 * (c & 3));
-    }
-    auto h = [&](uint32_t c) -> uint32_t { return (w[c >> 2] >> (8 * (c & 3))) & 0xFFu; };
-    ufc_item it{};
-    if (m == kItemsPos) {
-      uint32_t hs, dl;
-      ufc_codec::datagram_size(h, hs, dl);
-      ufc_codec::decode_datagram(h, hs, it);
-      it.data_offset = hoff + hs;
-    } else {
-      ufc_codec::decode_ack_group(h, it);
-    }
-    store_item<true>(items + wbase + g, it);
-  }
-  // Frames whose headers did not fit the slots: walked again by their own thread, items stored directly.
-  if (mode == kItemsWalk && first < cap) {
-    uint64_t aa;
-    const uint32_t len = frame_len32(offsets, i, aa);
-    const uint32_t room = (uint32_t)min((uint64_t)cnt, cap - first);
-    ufc_frame_info tmp;
-    ufc_codec::read_frame_to(DevBytes{bytes + aa}, len, valid[i] != 0, tmp, PackedSink{items + first}, room);
-  }
-}
-
 }  // namespace
 
 namespace {
@@ -711,15 +444,35 @@ size_t parse_scratch_bytes(uint64_t n, uint64_t items_cap) {
 hipError_t parse_batch(const ParseArgs& a, void* scratch, size_t scratch_bytes, hipStream_t stream) {
   const uint64_t n = a.n;
   const uint64_t blocks = (n + kParseThreads - 1) / kParseThreads;
-  // One pass (parse_fused_kernel): a tile counter and one look-back word per tile, zeroed first.
-  const size_t need = 256 + blocks * 8;
-  if (need > scratch_bytes) return hipErrorInvalidValue;
+  const ParseLayout lay(n, a.items_cap, scan_temp_bytes(n));
+  if (lay.end > scratch_bytes) return hipErrorInvalidValue;
   char* s = (char*)scratch;
-  hipError_t e = hipMemsetAsync(s, 0, need, stream);
+  uint32_t* counts = (uint32_t*)(s + lay.counts);
+  uint32_t* wg_counts = (uint32_t*)(s + lay.wg_counts);
+  uint32_t* wg_firsts = (uint32_t*)(s + lay.wg_firsts);
+  uint8_t* modes = (uint8_t*)(s + lay.modes);
+  unsigned long long* cursor = (unsigned long long*)(s + lay.cursor);
+  uint32_t* bases = (uint32_t*)(s + lay.bases);
+  uint16_t* pos_seg = (uint16_t*)(s + lay.slots);
+  void* temp = s + lay.temp;
+  size_t temp_bytes = lay.end - lay.temp;
+  hipError_t e = hipMemsetAsync(cursor, 0, 8, stream);
   if (e != hipSuccess) return e;
-  parse_fused_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, a.items,
-                                                                     a.items_cap, a.items_used, (uint32_t*)s,
-                                                                     (uint64_t*)(s + 256));
+  parse_walk_pool_kernel<<<(unsigned)blocks, kParseThreads, 0, stream>>>(a.bytes, a.offsets, n, a.valid, a.infos, counts,
+                                                                         modes, pos_seg, cursor, bases, lay.seg_cap,
+                                                                         wg_counts);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  // each workgroup's first item (the emit adds the frames' own counts within the workgroup)
+  e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, wg_counts, wg_firsts, (int)blocks, stream);
+  if (e != hipSuccess) return e;
+  // One item per thread per round, one non-temporal 16-byte load per header, non-temporal record
+  // stores (the measured alternatives in profiles/EXPERIMENTS.md).  (A one-launch
+  // parse -- walk, decoupled look-back scan and emit in one kernel -- measured 0.533 against 0.4206 ms
+  // here, round 5.)
+  parse_emit_kernel<1, 2, kEmitAux, true><<<(unsigned)blocks, kParseThreads, 0, stream>>>(
+      a.bytes, a.offsets, n, a.valid, a.infos, counts, wg_firsts, modes, pos_seg, bases, a.items, a.items_cap,
+      a.items_used);
   return hipGetLastError();
 }
 
