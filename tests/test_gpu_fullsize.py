@@ -189,19 +189,32 @@ def test_golden_reference_frames_fixture(engine):
     assert not v2.any()
 
 
-def test_parse_bench_workload_full(engine):
-    """The parse workload tools/bench_configs.py times (1M uflow frames, 1.41 GB: data frames with
-    micro/small/large datagrams, receive-side data frames and ack frames, 600 distinct frames from the
-    codec oracle tiled), with one bit flipped in every 997th frame: the GPU gate + GPU parse vs the
-    native host parse with its own host gate (ufc_parse_batch_host, pinned to the codec oracle by the
-    CPU suite), every info and every item compared."""
+def _parse_workload_base(mtu):
+    """tools/bench_configs.py's parse workloads: 600 distinct frames from the codec oracle (mtu: each data
+    frame cut to the datagrams that fit MAX_FRAME_SIZE)."""
     import random
     from oracle import codec as C
+    rng = random.Random(5)
+
+    def fit(fr):
+        while mtu and fr["kind"] == "data" and fr["datagrams"] and len(C.frame_write(fr)) > C.MAX_FRAME_SIZE:
+            fr["datagrams"].pop()
+        return C.frame_write(fr)
+    return [fit(C.random_data_frame(rng) if i % 3 == 0 else C.receive_side_data_frame(rng)
+                if i % 3 == 1 else C.random_ack_frame(rng, 20)) for i in range(600)]
+
+
+@pytest.mark.parametrize("mtu", [False, True], ids=["test_generators", "mtu"])
+def test_parse_bench_workload_full(engine, mtu):
+    """The parse workloads tools/bench_configs.py times (1M uflow frames: data frames with
+    micro/small/large datagrams, receive-side data frames and ack frames, 600 distinct frames from the
+    codec oracle tiled; 1.41 GB, or 0.60 GB with every frame <= MAX_FRAME_SIZE), with one bit flipped in
+    every 997th frame: the GPU gate + GPU parse vs the native host parse with its own host gate
+    (ufc_parse_batch_host, pinned to the codec oracle by the CPU suite), every info and every item
+    compared."""
     from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host
     n = 1_000_000
-    rng = random.Random(5)
-    base = [C.frame_write(C.random_data_frame(rng) if i % 3 == 0 else C.receive_side_data_frame(rng)
-                          if i % 3 == 1 else C.random_ack_frame(rng, 20)) for i in range(600)]
+    base = _parse_workload_base(mtu)
     lens = np.array([len(base[i % 600]) for i in range(n)], dtype=np.int64)
     offsets = np.zeros(n + 1, dtype=np.int64)
     offsets[1:] = np.cumsum(lens)
@@ -219,7 +232,7 @@ def test_parse_bench_workload_full(engine):
     got_items = _host(items[:k]).view(ITEM_DTYPE).reshape(-1)
     ref_infos, ref_items = parse_batch_host(data, offsets.astype(np.uint64), None, nthreads=THREADS)
     assert int(got_infos["crc_ok"].sum()) == n - flipped.size
-    assert k == ref_items.size and k > 14_000_000, k
+    assert k == ref_items.size and k > (11_000_000 if mtu else 14_000_000), k
     bad = np.nonzero((got_infos.view(np.uint8).reshape(n, -1) != ref_infos.view(np.uint8).reshape(n, -1)).any(1))[0]
     assert bad.size == 0, f"{bad.size} frame infos differ, first frames {bad[:8]}"
     bad = np.nonzero((got_items.view(np.uint8).reshape(k, -1) != ref_items.view(np.uint8).reshape(k, -1)).any(1))[0]

@@ -1,6 +1,6 @@
 """Secondary measurements for DESIGN.md (BASELINE.json configs 3, 4-per-GPU and 5, the seal and the
 parse), one JSON line each.  Not the driver's bench (bench.py is); run on the GPU box:
-    python tools/bench_configs.py [--only varlen,shard,seal,seal_varlen,parse,host] [--reps 20]
+    python tools/bench_configs.py [--only varlen,shard,seal,seal_varlen,parse,parse_mtu,host] [--reps 20]
 
   varlen   config 3: 10M frames, lengths U[64,1500] (splitmix64, seed 0x5EED0002), CSR offsets,
            device-resident; every frame checked against the oracle; CPU baseline of the same loop
@@ -8,7 +8,9 @@ parse), one JSON line each.  Not the driver's bench (bench.py is); run on the GP
   shard    config 4, one GPU's shard: frames [37.5M, 50M) of the 100M-frame batch (seed 0x5EED0003),
            18.75 GB device-resident (3 launches of the lean kernel).
   seal     the encode side of config 2: 1M x 1500-B frames sealed in place on the device.
-  parse    Frame::read past the gate on the device (ufc_parse_batch_varlen): 1M real uflow frames.
+  parse    Frame::read past the gate on the device (ufc_parse_batch_varlen): 1M real uflow frames from
+           the reference's test generators (38 % longer than MAX_FRAME_SIZE).
+  parse_mtu  the same with frames <= MAX_FRAME_SIZE only (what a uflow receiver gets).
   host     config 5's GPU leg: 1M x 1472-B frames (uflow's MAX_FRAME_SIZE) that start and end in
            host memory -> ufc_validate_host_varlen (H2D + CRC + D2H) from pinned and from pageable
            buffers; GiB/s of frame bytes including the copies.
@@ -208,14 +210,26 @@ def seal_varlen(eng, dev, reps, n=10_000_000):
                  valid_after_seal=ok)
 
 
-def parse(eng, dev, reps, n=1_000_000):
+def parse(eng, dev, reps, n=1_000_000, mtu=False):
     """ufc_parse_batch_varlen over n real uflow frames (data frames with datagrams, acks, syncs):
-    600 distinct frames from the codec oracle, tiled."""
+    600 distinct frames from the codec oracle, tiled.  The generators are the reference's test
+    generators (random_data_frame, serial/mod.rs:932-992), which ignore the frame size limit: 38 % of
+    these frames are longer than MAX_FRAME_SIZE (1472 B, src/lib.rs:291-294), up to 7.5 KB, and take
+    the gate's byte path.  mtu=True keeps only frames a uflow receiver can get (<= MAX_FRAME_SIZE: the
+    emitters' limit, half_connection/emit.rs:69, and the receive buffer, server/mod.rs:595): each data
+    frame keeps the longest prefix of its datagrams that fits, as the emitter packs a frame until the
+    next datagram would not fit (emit.rs:69)."""
     import random
     from oracle import codec as C
     rng = random.Random(5)
-    base = [C.frame_write(C.random_data_frame(rng) if i % 3 == 0 else C.receive_side_data_frame(rng)
-                          if i % 3 == 1 else C.random_ack_frame(rng, 20)) for i in range(600)]
+
+    def fit(fr):  # (data frames: drop datagrams from the end until the frame fits)
+        while mtu and fr["kind"] == "data" and fr["datagrams"] and len(C.frame_write(fr)) > C.MAX_FRAME_SIZE:
+            fr["datagrams"].pop()
+        return C.frame_write(fr)
+    base = [fit(C.random_data_frame(rng) if i % 3 == 0 else C.receive_side_data_frame(rng)
+                if i % 3 == 1 else C.random_ack_frame(rng, 20)) for i in range(600)]
+    assert not mtu or max(len(f) for f in base) <= C.MAX_FRAME_SIZE
     frames = [base[i % 600] for i in range(n)]
     lens = np.array([len(f) for f in frames], dtype=np.int64)
     offsets = np.zeros(n + 1, dtype=np.int64)
@@ -248,11 +262,17 @@ def parse(eng, dev, reps, n=1_000_000):
     # algorithmic bytes of the parse: the frame bytes read once, the offsets and
     # gate flags read, the 24-byte items and 32-byte infos written
     algo = total + 8 * (n + 1) + n + 24 * k + 32 * n
-    return {"config": "f3: device parse of 1M uflow frames after the gate", "frames": n,
+    return {"config": ("f3: device parse of 1M uflow frames <= MAX_FRAME_SIZE after the gate" if mtu else
+                       "f3: device parse of 1M uflow frames after the gate (test generators, 38 % over MAX_FRAME_SIZE)"),
+            "frames": n,
             "frame_bytes": total, "items": k, "items_digest": digest, "ms": round(med, 4), "mean_ms": round(mean, 4),
             "frames_per_s": round(n / med * 1e3), "GB_s_of_frame_bytes": round(total / med / 1e-3 / 1e9, 1),
             "algorithmic_bytes": algo, "frac_of_8TBs": round(algo / (med * 1e-3) / 8e12, 4),
             "gate_plus_parse_ms": round(med2, 4)}
+
+
+def parse_mtu(eng, dev, reps):
+    return parse(eng, dev, reps, mtu=True)
 
 
 def host(eng, reps=5, n=1_000_000, L=1472):
@@ -289,7 +309,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--varlen-kernel", default="auto", choices=["auto", "sorted8"],
                     help="variable-length kernel of the timed runs (the other one is timed beside it)")
-    ap.add_argument("--only", default="varlen,shard,seal,seal_varlen,parse,host")
+    ap.add_argument("--only", default="varlen,shard,seal,seal_varlen,parse,parse_mtu,host")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-check", action="store_true",
                     help="skip the oracle checks and CPU baselines (counter passes of tools/profile_workloads.sh)")

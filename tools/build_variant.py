@@ -2,7 +2,7 @@
 scratch tree, `file:old=>new` substitutions applied (each must match), compiled with the product's
 flags.  A/B measurement only (tools/ab_inproc.py); the product library is never touched.
 `file@path` replaces a source file of the copy with another file (e.g. an earlier round's, from git show);
-VARIANT_FLAGS (environment) adds hipcc flags.
+VARIANT_FLAGS (environment) adds hipcc flags; VARIANT_NO_MLLVM drops the named `-mllvm` options.
 Usage: python tools/build_variant.py <name> 'frame_crc_varlen8.hip:old=>new' 'frame_parse.hip@/tmp/old.hip' ..."""
 import os
 import shutil
@@ -34,6 +34,10 @@ def main():
         open(p, "w").write(s.replace(old, new))
     sources, flags, _ = _build._native_identity()
     flags = flags + os.environ.get("VARIANT_FLAGS", "").split()
+    for opt in os.environ.get("VARIANT_NO_MLLVM", "").split():
+        i = flags.index(opt)
+        assert flags[i - 1] == "-mllvm", opt
+        del flags[i - 1:i + 1]
     objs = []
     jobs = []
     for src in sources:

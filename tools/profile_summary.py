@@ -35,7 +35,10 @@ WORKLOADS = {
               N2 * (L2 + 4)),
              ("config 2 seal, two passes (comparison): pass 2 (trailer stores)", "seal_scatter_kernel", N2 * 8)],
     "seal_varlen": [("config 3 seal", "frame_crc_varlen8_kernel<true, false", "seal_varlen")],
-    "parse": [("parse, one launch (walk, look-back scan, item emit)", "parse_fused", "parse")],
+    "parse": [("parse walk (test-generator workload)", "parse_walk", None),
+              ("parse emit (test-generator workload)", "parse_emit", None)],
+    "parse_mtu": [("parse walk (frames <= MAX_FRAME_SIZE)", "parse_walk", None),
+                  ("parse emit (frames <= MAX_FRAME_SIZE)", "parse_emit", None)],
 }
 
 
@@ -79,7 +82,7 @@ def main():
             warm = d[5:] if len(d) > 10 else d  # (the first dispatches of a process run on a cold GPU)
             if algo == "varlen":
                 algo = line.get("algorithmic_bytes")
-            elif algo in ("seal_varlen", "parse"):
+            elif algo == "seal_varlen":
                 algo = line.get("algorithmic_bytes")
             fe = summarise(os.path.join(src, f"{w}_fetch"), sub).get("FETCH_SIZE", {})
             wr = summarise(os.path.join(src, f"{w}_write"), sub).get("WRITE_SIZE", {})

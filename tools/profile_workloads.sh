@@ -5,12 +5,12 @@
 #   <w>_fetch   rocprofv3 --pmc FETCH_SIZE            (own pass: FETCH uses 3 TCC counters)
 #   <w>_write   rocprofv3 --pmc WRITE_SIZE            (own pass)
 # workloads: bench (config 2, bench.py), varlen (config 3), shard (config 4's per-GPU share), seal,
-# seal_varlen, parse (tools/bench_configs.py --only <w>).  Each step has its own time limit; the
+# seal_varlen, parse, parse_mtu (tools/bench_configs.py --only <w>).  Each step has its own time limit; the
 # chain stops at the first failure.  Usage: tools/profile_workloads.sh <tag> [workloads]
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-prof}
-WL=${2:-bench varlen shard seal seal_varlen parse}
+WL=${2:-bench varlen shard seal seal_varlen parse parse_mtu}
 OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
