@@ -152,12 +152,21 @@ __device__ __forceinline__ void chain4(const Lane8& L, Chains& c, uint4 x) {
 // One line of a frame whose stream may end inside it: lim = bytes of the lane's 16 before the end of
 // the CRC'd data.  Words before the frame's end (the data's and the trailer's) step their slots,
 // the trailer's bytes and those past the data as zeros; words past the frame's end do not step.
+// The first lim bytes of a lane's 16 (lim clamped to 0..16), from the front-fix table: its entry n holds
+// the mask of bytes n .. 15 (fixtab_store: the frame's bytes, G's excluded), so the data mask is its
+// complement -- one ds_read_b128 and one bitop3 per word instead of a shift mask per word.
+__device__ __forceinline__ uint4 end_masked(const char* lds, uint4 x, int lim) {
+  const uint32_t i = (uint32_t)min(max(lim, 0), 16);
+  const uint4 m = *(const uint4*)(lds + fixtab_addr(i));
+  return make_uint4(x.x & ~m.x, x.y & ~m.y, x.z & ~m.z, x.w & ~m.w);
+}
+
 __device__ __forceinline__ void chain4_masked(const Lane8& L, Chains& c, uint4 x, int lim) {
-  const int b = 8 * lim;
-  const uint32_t n0 = chain_step(L.lds, c.v0, L.K, x.x & data_mask_bits(b));
-  const uint32_t n1 = chain_step(L.lds, c.v1, L.K, x.y & data_mask_bits(b - 32));
-  const uint32_t n2 = chain_step(L.lds, c.v2, L.K, x.z & data_mask_bits(b - 64));
-  const uint32_t n3 = chain_step(L.lds, c.v3, L.K, x.w & data_mask_bits(b - 96));
+  const uint4 d = end_masked(L.lds, x, lim);
+  const uint32_t n0 = chain_step(L.lds, c.v0, L.K, d.x);
+  const uint32_t n1 = chain_step(L.lds, c.v1, L.K, d.y);
+  const uint32_t n2 = chain_step(L.lds, c.v2, L.K, d.z);
+  const uint32_t n3 = chain_step(L.lds, c.v3, L.K, d.w);
   c.v0 = lim > -4 ? n0 : c.v0;
   c.v1 = lim > 0 ? n1 : c.v1;
   c.v2 = lim > 4 ? n2 : c.v2;
@@ -441,7 +450,10 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     }
 #pragma unroll
     for (int k = PART == 0 ? 1 : kV8Split; k < (PART == 0 ? kV8Split : kV8Pieces); k++) {
-      const uint32_t vo = (uint32_t)k + P >= 14u ? base : kV8Oob;
+      uint32_t vo = (uint32_t)k + P >= 14u ? base : kV8Oob;
+      // (opaque to the optimizer: otherwise it pushes the slot's constant 128 k through the select, one
+      // more add and one more register per slot, instead of the load's immediate offset)
+      asm("" : "+v"(vo));
       u32x4 v;
       if (k == kV8Pieces - 1)
         v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxShared);
@@ -510,11 +522,8 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     };
     Chains c{0u, 0u, 0u, 0u, 0u};
     auto masked_init = [&](uint4 x, int lim) {  // from zero chains: words past the end stay zero
-      const int bb = 8 * lim;
-      c.v0 = x.x & data_mask_bits(bb);
-      c.v1 = x.y & data_mask_bits(bb - 32);
-      c.v2 = x.z & data_mask_bits(bb - 64);
-      c.v3 = x.w & data_mask_bits(bb - 96);
+      const uint4 d = end_masked(L.lds, x, lim);
+      c = Chains{d.x, d.y, d.z, d.w, 0u};
     };
     auto entry = [&](int s) {
       const uint4 x = xin(s);
