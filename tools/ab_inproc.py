@@ -6,7 +6,7 @@ environment overrides (tuning builds, -DUFC_TUNING): each variant gets its own c
 with its overrides set (the kernel selection is read at ufc_ctx_create), and the overrides are
 also set around its launches (the few knobs read per launch, e.g. UFC_V8_WAVES):
 
-    python tools/ab_inproc.py [--varlen] name=lib.so[,ENV=VAL...] ...
+    python tools/ab_inproc.py [--varlen [--seal]] name=lib.so[,ENV=VAL...] ...
 
 Prints, per variant, the median over rounds of the per-round median kernel time (HIP events on
 the launch stream) and the min; validates the results of variants without an ablation.
@@ -51,6 +51,7 @@ def make_ctx(lib, env):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     varlen = "--varlen" in sys.argv
+    seal = "--seal" in sys.argv  # (with --varlen: time ufc_seal_batch_varlen instead of the gate)
     rounds = int(os.environ.get("AB_ROUNDS", 8))
     reps = int(os.environ.get("AB_REPS", 20))
     variants = []
@@ -97,7 +98,9 @@ def main():
                                         valid.data_ptr(), sp)
             assert r == 0
             return
-        if varlen:
+        if varlen and seal:  # (sealing in place again writes the same trailers)
+            r = lib.ufc_seal_batch_varlen(ctx, frames.data_ptr(), offs.data_ptr(), n, crc.data_ptr(), sp)
+        elif varlen:
             r = lib.ufc_crc_batch_varlen(ctx, frames.data_ptr(), offs.data_ptr(), n, crc.data_ptr(),
                                          valid.data_ptr(), sp)
         else:
@@ -143,6 +146,12 @@ def main():
                     del os.environ[k]
                 else:
                     os.environ[k] = v
+    if varlen and seal:  # every variant sealed the same bytes in place: they must still validate
+        lib0, ctx0 = libs[variants[0][0]]
+        assert lib0.ufc_crc_batch_varlen(ctx0, frames.data_ptr(), offs.data_ptr(), n, crc.data_ptr(), valid.data_ptr(),
+                                         sp) == 0
+        torch.cuda.synchronize()
+        print(f"# after every variant's seals: {int(valid.sum().item())} of {n} frames valid", flush=True)
     for name, _, _ in variants:
         t = np.array(times[name])
         print(f"{name:24s} median {np.median(t):.4f} ms  min {t.min():.4f}  max {t.max():.4f}  "
