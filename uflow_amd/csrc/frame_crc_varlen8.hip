@@ -19,9 +19,13 @@
 //     product.  Words past a frame's end step nothing; the bytes past its data are masked out.
 //   * Slots run right-aligned: position s = 0 .. 12 holds line s - 13 + P, so every frame's last line
 //     is at position 12 and the lines before a frame's first are zeros (chains stay zero).  A set runs
-//     positions 13 - Pmax .. 12 straight through, entered by one switch on its longest frame; line 0
-//     (slot 0, loaded apart for its cache policy) goes in at position 13 - P.  Only positions 11 and
-//     12 can need masked steps.
+//     positions 13 - Pmax .. 12 straight through (one copy of the sequence per entry point, chosen by a
+//     switch on its longest frame); line 0 (slot 0, loaded apart for its cache policy) goes in at
+//     position 13 - P.  Only positions 11 and 12 can need masked steps.
+//   * One set buffer per wave, software-pipelined: each slot of the next set is issued as soon as the
+//     current set has consumed that slot's registers (126 VGPRs: 16 waves per CU).  The straight copy
+//     per entry point keeps the order of those loads the same on every path, so the compiler's load
+//     waits stay counted (with one shared sequence it waited for every load at each entry point).
 //   * Sets come from runs of 64 frames sorted by line count in the wave that takes them (four one-bit
 //     radix split passes); the per-set facts come once per run from half-row reductions and ballots.
 //   * Results of a run (8 sets x 8 frames) collect in one register pair per lane and leave with
@@ -39,7 +43,6 @@ namespace ufc_dev {
 namespace {
 
 constexpr int kV8Pieces = 13;              // fast path: windows of up to 13 lines (frames of 4..1532 B)
-constexpr int kV8Split = 7;                // slots 0 .. 6 in a set's first load part, 7 .. 12 in its second
 constexpr uint32_t kV8Bias = 0x20000;      // window offsets: relative to the run's base - bias
 constexpr uint32_t kV8Oob = 0x80000000u;   // out-of-range offset: zeros, no memory request
 constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay below this
@@ -233,15 +236,15 @@ struct Buf13 {
 
 }  // namespace
 
-// One workgroup of kV8Waves waves per CU, 2 sets per wave in the ring (the set computed plus one in
-// flight).  p.offsets = the CSR offsets (n + 1) or, with PAIRS, the (start, end) pairs (p.frame_len =
-// the buffer length).  Each run of 64 frames is ordered by block count in the wave that takes it,
-// after each frame's fast-path geometry has been computed in the frame's own lane; the per-set
-// facts (max block count, mixed counts, byte path, G in block 1) come once per run from half-row
-// DPP reductions and ballots, and a set takes its two words per group with ds_bpermute and its
-// set-level bits with one readfirstlane.  Frames the fast path cannot take sort together (key 7),
-// so they spoil fewer sets.
-constexpr int kV8Waves = 12;
+// One workgroup of kV8Waves waves per CU (126 VGPRs: 4 waves per SIMD), one set buffer per wave,
+// software-pipelined: the next set's slots are issued into the registers the current set has just
+// consumed.  p.offsets = the CSR offsets (n + 1) or, with PAIRS, the (start, end) pairs (p.frame_len =
+// the buffer length).  Each run of 64 frames is ordered by line count in the wave that takes it,
+// after each frame's fast-path geometry has been computed in the frame's own lane; the per-set facts
+// come once per run from half-row DPP reductions and ballots, and a set takes its two words per group
+// with ds_bpermute and its set-level bits with one readfirstlane.  Frames the fast path cannot take
+// sort together (key 14), so they spoil fewer sets.
+constexpr int kV8Waves = 16;
 template <bool SEAL, bool PAIRS>
 __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const KernelParams p) {
   constexpr int WAVES = kV8Waves;
@@ -433,43 +436,38 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // The set's loads (struct Buf13): line 0 (slot 0) and the last line (slot 12), the lines the frame
   // shares with its neighbours (which the sort puts in other sets), with default policy so that they
   // stay in L2 for them; the lines in between, each read by this set alone, non-temporal; lanes wholly
-  // before G and slots before a frame's line 1 are out of range (zeros, no request).  Then the trailer,
-  // one dword at zo.  Issued in two parts (PART 0: slots 0 .. kV8Split - 1 and the trailer; PART 1:
-  // the rest), the second during the previous set's compute, once its early slots' registers are free.
-  auto load_set = [&](uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b, auto part) {
-    constexpr int PART = decltype(part)::value;
+  // before G and slots before a frame's line 1 are out of range (zeros, no request); the trailer, one
+  // dword at zo.  Slot k of a set (k = 0: line 0; k >= 1: line k - 13 + P, out of range before line 1)
+  // is issued one at a time, as the current set frees the slot's registers.
+  auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b) {
     const uint32_t P = w_P(geo), front = w_r(geo) + 4u;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
-    // slot s at base + 128 s (line s - 13 + P); (an out-of-range voff0 keeps base out of range for every
-    // slot it is used in: s + P >= 14; the run base's bias keeps base itself above 0)
-    const uint32_t base = voff0 + 128u * P - 128u * 13u;
-    if constexpr (PART == 0) {
+    if (k == 0) {
       const uint32_t vo = (16u * L.col + 16u <= front) ? kV8Oob : voff0;
       const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8AuxShared);
       b.x[0] = make_uint4(v.x, v.y, v.z, v.w);
+      return;
     }
-#pragma unroll
-    for (int k = PART == 0 ? 1 : kV8Split; k < (PART == 0 ? kV8Split : kV8Pieces); k++) {
-      uint32_t vo = (uint32_t)k + P >= 14u ? base : kV8Oob;
-      // (opaque to the optimizer: otherwise it pushes the slot's constant 128 k through the select, one
-      // more add and one more register per slot, instead of the load's immediate offset)
-      asm("" : "+v"(vo));
-      u32x4 v;
-      if (k == kV8Pieces - 1)
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxShared);
-      else
-        v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxInterior);
-      b.x[k] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-    if constexpr (PART == 0) {
-      if constexpr (!SEAL) {
-        const uint32_t vt = voff0 == kV8Oob ? kV8Oob : voff0 - 16u * L.col + w_zo(geo);
-        b.tr = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vt, 0, kV8AuxShared);
-      }
-    }
+    // slot k at base + 128 k (an out-of-range voff0 keeps base out of range wherever it is used:
+    // k + P >= 14; the run base's bias keeps base itself above 0)
+    const uint32_t base = voff0 + 128u * P - 128u * 13u;
+    uint32_t vo = (uint32_t)k + P >= 14u ? base : kV8Oob;
+    // (opaque to the optimizer: otherwise it pushes the slot's constant 128 k through the select, one
+    // more add and one more register per slot, instead of the load's immediate offset)
+    asm("" : "+v"(vo));
+    u32x4 v;
+    if (k == kV8Pieces - 1)
+      v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxShared);
+    else
+      v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxInterior);
+    b.x[k] = make_uint4(v.x, v.y, v.z, v.w);
   };
-  using Part0 = std::integral_constant<int, 0>;
-  using Part1 = std::integral_constant<int, 1>;
+  auto load_tr = [&](uint32_t voff0, uint32_t geo, uint64_t sb) -> uint32_t {
+    if constexpr (SEAL) return 0u;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
+    const uint32_t vt = voff0 == kV8Oob ? kV8Oob : voff0 - 16u * L.col + w_zo(geo);
+    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vt, 0, kV8AuxShared);
+  };
 
   // ---- results of the current run: lane (g, col = t) <- set t's frame g; qv = orig | valid << 31
   uint32_t acc_crc = 0, acc_qv = 0;
@@ -502,13 +500,15 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // chains at zero: the set runs positions 13 - Pmax .. 12 straight through, every lane stepping at
   // every position, entered once by a switch on Pmax (one merge of the chain registers per set).  Only
   // positions 11 and 12 (lines P - 2 and P - 1) can hold bytes past the CRC'd data (masked steps).
-  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf13& b, uint32_t voff0, uint64_t sb, auto mid) {
-    static_assert(kV8Split == 7 && kV8Pieces == 13, "the position sequence below");
+  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf13& b, uint32_t tr, uint32_t voff0, uint64_t sb,
+                     auto issue) {
+    static_assert(kV8Pieces == 13, "the position sequence below");
     const uint32_t zo = w_zo(geo), P = w_P(geo), front = w_r(geo) + 4u;
     const int lim0 = (int)zo - (int)(16u * L.col);
     const int lim12 = lim0 - 128 * (int)(P - 1u), lim11 = lim12 + 128;
     const int g1 = 128 + (int)(16u * L.col) - (int)front;  // G's last bytes in line 1 (r >= 125)
     const uint4 fx = fix_piece(L.lds, b.x[0], (int)front - (int)(16u * L.col));  // line 0
+    issue(0);
     const uint32_t Iend = 13u - m.Pmin;  // positions holding some frame's line 0: 13 - Pmax .. Iend
     auto xin = [&](int s) -> uint4 {  // position s's piece
       uint4 x = s == 0 ? make_uint4(0u, 0u, 0u, 0u) : b.x[s];
@@ -526,6 +526,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
       c = Chains{d.x, d.y, d.z, d.w, 0u};
     };
     auto entry = [&](int s) {
+      for (int k = 1; k < s; k++) issue(k);  // (slots this set does not use)
       const uint4 x = xin(s);
       if (s == 12)
         masked_init(x, lim12);
@@ -533,6 +534,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
         masked_init(x, lim11);
       else
         c = Chains{x.x, x.y, x.z, x.w, 0u};
+      if (s > 0) issue(s);
     };
     auto stepk = [&](int s) {
       const uint4 x = xin(s);
@@ -542,44 +544,34 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
         chain4_masked(L, c, x, lim11);
       else
         chain4(L, c, x);
+      issue(s);
     };
-    auto midk = [&]() {  // the next set's second part: slots 1 .. kV8Split - 1 of this one are done
-      __builtin_amdgcn_sched_barrier(0);
-      mid();
-      __builtin_amdgcn_sched_barrier(0);
+    // one straight copy of the positions per entry point (no merges inside: the loads the positions
+    // issue keep one order on every path, so their waits stay counted)
+    auto from = [&](auto e) {
+      constexpr int E = decltype(e)::value;
+      entry(E);
+#pragma unroll
+      for (int k = E + 1; k <= 12; k++) stepk(k);
     };
     switch (m.Pmax) {  // enter at position 13 - Pmax
-      case 13: entry(0); goto p1;
-      case 12: entry(1); goto p2;
-      case 11: entry(2); goto p3;
-      case 10: entry(3); goto p4;
-      case 9: entry(4); goto p5;
-      case 8: entry(5); goto p6;
-      case 7: entry(6); goto p7;
-      case 6: entry(7); midk(); goto p8;
-      case 5: entry(8); midk(); goto p9;
-      case 4: entry(9); midk(); goto p10;
-      case 3: entry(10); midk(); goto p11;
-      case 2: entry(11); midk(); goto p12;
-      default: entry(12); midk(); goto p13;
+      case 13: from(std::integral_constant<int, 0>{}); break;
+      case 12: from(std::integral_constant<int, 1>{}); break;
+      case 11: from(std::integral_constant<int, 2>{}); break;
+      case 10: from(std::integral_constant<int, 3>{}); break;
+      case 9: from(std::integral_constant<int, 4>{}); break;
+      case 8: from(std::integral_constant<int, 5>{}); break;
+      case 7: from(std::integral_constant<int, 6>{}); break;
+      case 6: from(std::integral_constant<int, 7>{}); break;
+      case 5: from(std::integral_constant<int, 8>{}); break;
+      case 4: from(std::integral_constant<int, 9>{}); break;
+      case 3: from(std::integral_constant<int, 10>{}); break;
+      case 2: from(std::integral_constant<int, 11>{}); break;
+      default: from(std::integral_constant<int, 12>{}); break;
     }
-  p1: stepk(1);
-  p2: stepk(2);
-  p3: stepk(3);
-  p4: stepk(4);
-  p5: stepk(5);
-  p6: stepk(6);
-  p7: midk();
-    stepk(7);
-  p8: stepk(8);
-  p9: stepk(9);
-  p10: stepk(10);
-  p11: stepk(11);
-  p12: stepk(12);
-  p13:
     const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
     const uint32_t crc = ~unshift(group_lin8_rot(L, c, e), t);
-    const uint32_t ok = (!SEAL && w_len(geo) >= 5u && __builtin_bswap32(b.tr) == crc) ? 1u : 0u;
+    const uint32_t ok = (!SEAL && w_len(geo) >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     if (SEAL && L.col == 0u) {  // BE32 trailer: one (unaligned) dword store per frame
       // (non-temporal trailer stores measured slower: 1.912 against 1.874 ms)
       uint32_t* const ta = (uint32_t*)((uint8_t*)p.wbytes + sb + (voff0 + zo));
@@ -649,33 +641,23 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no visible load or store stays pending
   };
 
-  // ---- ring: set S_k in slot k % DEPTH; records DEPTH sets ahead of their geometry ----
-  constexpr int DEPTH = 2;
-  Buf13 B[DEPTH];
-  Rec O[DEPTH];
-  uint32_t GE[DEPTH], VO[DEPTH], QO[DEPTH], QG[DEPTH];  // set of O[i] / of GE[i], B[i]
-  uint64_t SB[DEPTH];
-  Set8Meta M[DEPTH];
-  // prologue: records of the wave's first 2 DEPTH - 1 sets, geometry + loads of the first
-  // DEPTH - 1 (all in the wave's first run, which needs no claim: 2 DEPTH - 1 <= 8)
-  Rec Rq[DEPTH];
-  uint32_t Qq[DEPTH];
+  // ---- software pipeline over one buffer: set S computes while set S + 1's slots are issued into
+  // the registers S has just consumed; records one set ahead of their geometry ----
+  Buf13 B;
+  Rec O;  // record of set QO
+  uint32_t QO, QG, GE, VO, TR;  // QG: the set being computed (its geometry GE, VO, SB, M, trailer TR)
+  uint64_t SB;
+  Set8Meta M;
+  {  // prologue: the first set's geometry and loads, the second set's record
+    QG = next_q();
+    const Rec r0 = load_rec(QG);
+    GE = geometry(QG, r0, VO, M, SB);
+    TR = load_tr(VO, GE, SB);  // (the loop's order: the trailer, then the slots)
 #pragma unroll
-  for (int i = 0; i < DEPTH; i++) {
-    Qq[i] = next_q();
-    Rq[i] = load_rec(Qq[i]);
+    for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, B);
+    QO = next_q();
+    O = load_rec(QO);
   }
-#pragma unroll
-  for (int i = 0; i < DEPTH - 1; i++) {
-    QG[i] = Qq[i];
-    GE[i] = geometry(QG[i], Rq[i], VO[i], M[i], SB[i]);
-    load_set(VO[i], GE[i], SB[i], B[i], Part0{});
-    load_set(VO[i], GE[i], SB[i], B[i], Part1{});
-    QO[i] = next_q();
-    O[i] = load_rec(QO[i]);
-  }
-  O[DEPTH - 1] = Rq[DEPTH - 1];
-  QO[DEPTH - 1] = Qq[DEPTH - 1];
   stage_store<WAVES * 64>(sr, lds);
   fixtab_store(lds, p.G);  // (then an LDS-only barrier, as in stage_store: the prefetches stay in flight)
   // Runs WR0 .. WR0 + WAVES - 1 are taken statically.  (Set by the thread whose stage_store wrote
@@ -686,35 +668,39 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
   claim_next();  // the second run (the counter is set now)
 
-  // One step: geometry + loads of set S + DEPTH - 1 (record loaded DEPTH steps ago), the record of
-  // set S + 2 DEPTH - 1, then compute set S.
-  auto step = [&](int cs, int fs) {
-    QG[fs] = QO[fs];
-    GE[fs] = geometry(QG[fs], O[fs], VO[fs], M[fs], SB[fs]);
-    load_set(VO[fs], GE[fs], SB[fs], B[fs], Part0{});
-    QO[fs] = next_q();
-    O[fs] = load_rec(QO[fs]);
+  // (a wave's sets are valid up to its first kNoSet)
+  while (QG != kNoSet) {
+    // the next set: geometry from its record, its trailer; the record after it
+    uint32_t VN;
+    uint64_t SBN;
+    Set8Meta MN;
+    const uint32_t QN = QO;
+    const uint32_t GN = geometry(QN, O, VN, MN, SBN);
+    const uint32_t TRN = load_tr(VN, GN, SBN);
+    QO = next_q();
+    O = load_rec(QO);
     __builtin_amdgcn_sched_barrier(0);
-    auto second = [&]() { load_set(VO[fs], GE[fs], SB[fs], B[fs], Part1{}); };
-    if (QG[cs] != kNoSet && !M[cs].slow) {
-      compute(QG[cs], GE[cs], M[cs], B[cs], VO[cs], SB[cs], second);
+    auto issue = [&](int k) { load_slot(k, VN, GN, SBN, B); };
+    if (!M.slow) {
+      compute(QG, GE, M, B, TR, VO, SB, issue);
     } else {
-      second();
-      if (QG[cs] != kNoSet) slow_set(QG[cs]);
+#pragma unroll
+      for (int k = 0; k < kV8Pieces; k++) issue(k);
+      slow_set(QG);
     }
     __builtin_amdgcn_sched_barrier(0);
-  };
-  // (a wave's sets are valid up to its first kNoSet, so a round stops at the first dead set)
-  while (QG[0] != kNoSet) {
-    step(0, 1);
-    step(1, 0);
+    QG = QN;
+    GE = GN;
+    VO = VN;
+    SB = SBN;
+    M = MN;
+    TR = TRN;
   }
 }
 
-// Product: 12 waves, 2 sets per wave in the ring (three waves per SIMD; config 3 1.69 ms kernel
-// against 1.93 ms at 8 waves / depth 3 and 2.4-2.6 ms at 14-16 waves, which spill), runs sorted in
-// the kernel with per-run geometry (1.480 against 1.506 ms with per-set geometry, config 3,
-// in-process A/B, identical results; profiles/EXPERIMENTS.md).
+// Product (round 5): 16 waves, one pipelined buffer each, one straight copy of the positions per entry
+// point (1.4337 against 1.4723 ms for 12 waves with two buffers each, config 3, in-process A/B,
+// identical results; profiles/EXPERIMENTS.md).
 template __global__ void frame_crc_varlen8_kernel<false, false>(const KernelParams);
 template __global__ void frame_crc_varlen8_kernel<true, false>(const KernelParams);
 template __global__ void frame_crc_varlen8_kernel<false, true>(const KernelParams);
