@@ -95,8 +95,7 @@ __device__ __forceinline__ uint32_t group_lin8(const Lane8& L, const Chains& c) 
   uint32_t K2 = 0;  // byte i = column*4 of the slot word multiplied in nibble step i (column = slot)
 #pragma unroll
   for (uint32_t i = 0; i < 4; i++) K2 |= ((4u * L.col + ((i + L.rot) & 3u)) * 4u) << (8 * i);
-  uint32_t v = xor3(nib_mul<0>(L.lds, X0, K2), nib_mul<1>(L.lds, X1, K2), nib_mul<2>(L.lds, X2, K2)) ^
-               nib_mul<3>(L.lds, X3, K2);
+  uint32_t v = nib_mul4(L.lds, X0, X1, X2, X3, K2);
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
@@ -114,8 +113,7 @@ __device__ __forceinline__ uint32_t group_lin8_rot(const Lane8& L, const Chains&
   const uint32_t a01 = r1 ? c.v1 : c.v0, a12 = r1 ? c.v2 : c.v1, a23 = r1 ? c.v3 : c.v2, a30 = r1 ? c.v0 : c.v3;
   const uint32_t X0 = r2 ? a23 : a01, X1 = r2 ? a30 : a12, X2 = r2 ? a01 : a23, X3 = r2 ? a12 : a30;
   const uint32_t K2 = rot_nibble_key(L.col, u, e);
-  uint32_t v = xor3(nib_mul<0>(L.lds, X0, K2), nib_mul<1>(L.lds, X1, K2), nib_mul<2>(L.lds, X2, K2)) ^
-               nib_mul<3>(L.lds, X3, K2);
+  uint32_t v = nib_mul4(L.lds, X0, X1, X2, X3, K2);
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
