@@ -166,9 +166,10 @@ void build_nibble_image32(uint32_t out[8192]) {
         uint32_t v = 0;
         if (c < 32) {
           v = advance((uint32_t)e << (4 * k), (uint64_t)4 * (31 - c));
-        } else if (c >= 40 && c < 52) {  // A^-8t for t = 1..3, one copy per 8-lane group mod 4
-          const int t = (c - 40) % 3 + 1;
-          v = retreat((uint32_t)e << (4 * k), (uint64_t)t);
+        } else if (k >= 2 && k <= 4) {  // A^-t (t = k - 1 bytes) of nibble (c - 32) & 7 alone: column
+          // 32 + l belongs to lane l of a half-wave, which looks up its own nibble (rows 0..31 of
+          // columns 32..39 hold the front-fix table, row 127 of column 63 the run counter)
+          v = retreat((uint32_t)e << (4 * ((c - 32) & 7)), (uint64_t)(k - 1));
         }
         out[(k * 16 + e) * 64 + c] = v;
       }

@@ -15,8 +15,8 @@
 //     frame's end (profiles/EXPERIMENTS.md, round 5).
 //   * Each lane's 4 words are 4 slot chains with the constant A^128 (32 slots per frame); the stream
 //     ends at the word holding the frame's last byte (slot e, t = 0..3 bytes past the frame), so the
-//     finish takes the slot constants rotated by e (group_lin8_rot) and undoes A^t with one nibble-table
-//     product.  Words past a frame's end step nothing; the bytes past its data are masked out.
+//     finish takes the slot constants rotated by e (group_lin8_rot) and undoes A^t with one nibble
+//     lookup per lane (its own nibble of lin) summed over the group.  Words past a frame's end step nothing; the bytes past its data are masked out.
 //   * Slots run right-aligned: position s = 0 .. 12 holds line s - 13 + P, so every frame's last line
 //     is at position 12 and the lines before a frame's first are zeros (chains stay zero).  A set runs
 //     positions 13 - Pmax .. 12 straight through (one copy of the sequence per entry point, chosen by a
@@ -49,7 +49,8 @@ constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay bel
 constexpr int kV8AuxShared = 0;            // a frame's first and last line: default policy (shared)
 constexpr int kV8AuxInterior = 2;          // the lines in between: non-temporal (read once)
 constexpr uint32_t kNoSet = 0xFFFFFFFFu;   // a wave's set sequence past its last claimed run
-// The workgroup's run counter: nibble-image row 127, column 63 (columns 52..63 are never read).
+// The workgroup's run counter: nibble-image row 127, column 63 (rows 80..127 of columns 32..63 are
+// never read).
 constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
 
 // Per-lane geometry of a frame on the fast path (one VGPR): r = (frame start - 4) mod 128 [0,7) (the
@@ -123,7 +124,8 @@ __device__ __forceinline__ uint32_t group_lin8_rot(const Lane8& L, const Chains&
 // Front-fix table in LDS: for p = 0..20 bytes of a 16-byte piece before its frame, the mask M of
 // the frame's bytes and the bytes Gs of G placed before them, so that front_fix(x, p, G) =
 // (x & M) | Gs (p <= 0: nothing to fix, p >= 20: all zero).  32 bytes per entry, in the unused
-// columns 32..39 of the 32-slot nibble image's rows 0..20 (columns 40..51 hold the A^-t tables).
+// columns 32..39 of the 32-slot nibble image's rows 0..20 (rows 32..79 of columns 32..63 hold the
+// A^-t tables).
 constexpr int kFixEntries = 21;
 __device__ __forceinline__ uint32_t fixtab_addr(uint32_t i) { return i * 256u + 128u; }
 
@@ -480,12 +482,16 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
       if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_qv >> 31);
     }
   };
-  // A^-t of every group's lin (the 32-slot image's columns 40 + 3 (g & 3) + t - 1 hold the nibble
-  // tables, one copy per group of a half-wave: no bank conflicts).
+  // A^-t of every group's lin, one nibble per lane: lane col of a group looks up A^-t of lin's nibble
+  // col in its own column 32 + (lane & 31) of the 32-slot image (rows 16 (t + 1) + nibble value; a
+  // half-wave's 32 lanes read 32 banks) and the group sums its 8 terms over DPP.
   auto unshift = [&](uint32_t lin, uint32_t t) -> uint32_t {
     if (__builtin_amdgcn_ballot_w64(t != 0) == 0) return lin;
-    const uint32_t col = 40u + 3u * (L.grp & 3u) + (t ? t - 1u : 0u);
-    const uint32_t r = nib_mul<0>(L.lds, lin, col * 4u);
+    const uint32_t nib = (lin >> (4u * L.col)) & 15u;
+    uint32_t r = *(const uint32_t*)(L.lds + ((t << 12) | (nib << 8)) + (L.K & 0xFFu) + (4096u + 128u));
+    r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);  // row_half_mirror
     return t ? r : lin;
   };
 
