@@ -210,6 +210,27 @@ def test_seal_varlen_large(engine):
     assert np.array_equal(crc_out.cpu().numpy().view(np.uint32), ref_crc)
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3, 37, 64])
+def test_seal_varlen_shared_blocks(engine, shift):
+    """The seal writes a trailer as its whole 64-byte block only where no other frame's trailer can
+    share the block: short neighbours (trailers a few bytes apart), frames whose block reaches back
+    before their start, trailers across a block edge, a batch at any address (blocks are aligned in
+    memory, not to the batch), and the bytes around the batch left alone."""
+    rng = np.random.default_rng(60 + shift)
+    lens = np.concatenate([rng.integers(4, 140, size=40_000), rng.integers(4, 1533, size=20_000),
+                           rng.integers(60, 70, size=5_000)])
+    rng.shuffle(lens)
+    offsets = np.zeros(len(lens) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    data = _rand_bytes(rng, int(offsets[-1]) + shift + 256)
+    ref = data.copy()
+    oracle.seal_varlen(ref[shift:shift + int(offsets[-1])], offsets.astype(np.uint64))
+    d = torch.from_numpy(data).to(DEV)
+    engine.seal_varlen(d[shift:shift + int(offsets[-1])], torch.from_numpy(offsets).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(d.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_varlen_misaligned_base(engine, shift):
     """The batch starts at an odd address (a view into a larger buffer): the kernel realigns its

@@ -8,7 +8,10 @@
 //   aligned     a dword store at the trailer rounded down to 4 B (wrong bytes: cost only);
 //   aligned x2  the two aligned dwords covering the trailer (one dwordx2 store);
 //   fixed       a dword store at every 1500th byte's trailer of a 1M-frame batch (config 2's pattern)
-//               for the per-write rate of the fixed seal.
+//               for the per-write rate of the fixed seal;
+//   block B     the whole aligned B-byte block (B = 16, 32, 64, 128) holding the trailer's first byte,
+//               B / 16 lanes per frame, one dwordx4 each (does a full-sector write skip the memory's
+//               read-modify-write of a partial one?).
 // Prints one line per variant (median of 9 launches; writes per second).
 #include <hip/hip_runtime.h>
 
@@ -40,6 +43,16 @@ __global__ void w_fixed(uint8_t* bytes, uint32_t n) {
   if (i < n) *(uint32_t*)(bytes + (uint64_t)i * 1500 + 1496) = 0x11A6F2A3u ^ i;
 }
 
+template <int B>
+__global__ void w_block(uint8_t* bytes, const uint64_t* off, uint32_t n) {
+  constexpr uint32_t T = B / 16;
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, i = g / T, c = g % T;
+  if (i < n) {
+    uint8_t* a = bytes + ((off[i + 1] - 4) & ~(uint64_t)(B - 1)) + 16 * c;
+    *(uint4*)a = make_uint4(i, ~i, c, 0x11A6F2A3u);
+  }
+}
+
 int main() {
   const uint32_t n = 10000000;
   std::vector<uint64_t> off(n + 1, 0);
@@ -60,13 +73,18 @@ int main() {
     const char* name;
     uint32_t writes;
     int k;
-  } vs[] = {{"unaligned", n, 0}, {"aligned", n, 1}, {"aligned x2", n, 2}, {"fixed 1M x 1500", nf, 3}};
+  } vs[] = {{"unaligned", n, 0}, {"aligned", n, 1}, {"aligned x2", n, 2}, {"fixed 1M x 1500", nf, 3},
+                {"block 16", n, 16}, {"block 32", n, 32}, {"block 64", n, 64}, {"block 128", n, 128}};
   auto launch = [&](int k) {
     switch (k) {
       case 0: hipLaunchKernelGGL(w_unaligned, dim3((n + 255) / 256), dim3(256), 0, 0, bytes, doff, n); break;
       case 1: hipLaunchKernelGGL(w_aligned, dim3((n + 255) / 256), dim3(256), 0, 0, bytes, doff, n); break;
       case 2: hipLaunchKernelGGL(w_aligned2, dim3((n + 255) / 256), dim3(256), 0, 0, bytes, doff, n); break;
-      default: hipLaunchKernelGGL(w_fixed, dim3((nf + 255) / 256), dim3(256), 0, 0, bytes, nf); break;
+      case 3: hipLaunchKernelGGL(w_fixed, dim3((nf + 255) / 256), dim3(256), 0, 0, bytes, nf); break;
+      case 16: hipLaunchKernelGGL(w_block<16>, dim3((n + 255) / 256), dim3(256), 0, 0, bytes, doff, n); break;
+      case 32: hipLaunchKernelGGL(w_block<32>, dim3((2 * n + 255) / 256), dim3(256), 0, 0, bytes, doff, n); break;
+      case 64: hipLaunchKernelGGL(w_block<64>, dim3((4 * n + 255) / 256), dim3(256), 0, 0, bytes, doff, n); break;
+      default: hipLaunchKernelGGL(w_block<128>, dim3((8 * n + 255) / 256), dim3(256), 0, 0, bytes, doff, n); break;
     }
   };
   hipEvent_t e0, e1;
