@@ -210,6 +210,30 @@ def test_seal_varlen_large(engine):
     assert np.array_equal(crc_out.cpu().numpy().view(np.uint32), ref_crc)
 
 
+@pytest.mark.parametrize("shift", [0, 1, 2, 3])
+def test_varlen_trailer_bytes(engine, shift):
+    """The gate reads each trailer from its frame's last two lines (no load of its own): one trailer
+    byte flipped in every third frame, each of the 4 bytes in turn, at every trailer position in a
+    line (those starting in the previous line's last word included)."""
+    rng = np.random.default_rng(70 + shift)
+    lens = rng.integers(4, 1533, size=60_000)
+    offsets = np.zeros(len(lens) + 1, dtype=np.int64)
+    offsets[1:] = np.cumsum(lens)
+    data = _rand_bytes(rng, int(offsets[-1]) + shift)
+    view = data[shift:]
+    oracle.seal_varlen(view, offsets.astype(np.uint64))
+    for i in range(0, len(lens), 3):
+        view[offsets[i + 1] - 4 + (i // 3) % 4] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    ref_crc, ref_valid = oracle.validate_varlen(view, offsets.astype(np.uint64))
+    d = torch.from_numpy(data).to(DEV)[shift:]
+    crc, valid = engine.crc_varlen(d, torch.from_numpy(offsets).to(DEV))
+    torch.cuda.synchronize()
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc)
+    assert np.array_equal(valid.cpu().numpy(), ref_valid)
+    ends = ((offsets[1:] + shift - 4) % 128).astype(np.int64)  # trailer start's line offset
+    assert {124, 125, 126, 127} <= set(ends[lens >= 5].tolist())
+
+
 @pytest.mark.parametrize("shift", [0, 1, 3, 37, 64])
 def test_seal_varlen_shared_blocks(engine, shift):
     """The seal writes a trailer as its whole 64-byte block only where no other frame's trailer can

@@ -436,9 +436,9 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // The set's loads (struct Buf13): line 0 (slot 0) and the last line (slot 12), the lines the frame
   // shares with its neighbours (which the sort puts in other sets), with default policy so that they
   // stay in L2 for them; the lines in between, each read by this set alone, non-temporal; lanes wholly
-  // before G and slots before a frame's line 1 are out of range (zeros, no request); the trailer, one
-  // dword at zo.  Slot k of a set (k = 0: line 0; k >= 1: line k - 13 + P, out of range before line 1)
-  // is issued one at a time, as the current set frees the slot's registers.
+  // before G and slots before a frame's line 1 are out of range (zeros, no request).  Slot k of a set
+  // (k = 0: line 0; k >= 1: line k - 13 + P, out of range before line 1) is issued one at a time, as
+  // the current set frees the slot's registers.
   auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b) {
     const uint32_t P = w_P(geo), front = w_r(geo) + 4u;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
@@ -461,12 +461,6 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     else
       v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxInterior);
     b.x[k] = make_uint4(v.x, v.y, v.z, v.w);
-  };
-  auto load_tr = [&](uint32_t voff0, uint32_t geo, uint64_t sb) -> uint32_t {
-    if constexpr (SEAL) return 0u;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
-    const uint32_t vt = voff0 == kV8Oob ? kV8Oob : voff0 - 16u * L.col + w_zo(geo);
-    return __builtin_amdgcn_raw_buffer_load_b32(rs, (int)vt, 0, kV8AuxShared);
   };
 
   // ---- results of the current run: lane (g, col = t) <- set t's frame g; qv = orig | valid << 31
@@ -504,7 +498,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // chains at zero: the set runs positions 13 - Pmax .. 12 straight through, every lane stepping at
   // every position, entered once by a switch on Pmax (one merge of the chain registers per set).  Only
   // positions 11 and 12 (lines P - 2 and P - 1) can hold bytes past the CRC'd data (masked steps).
-  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf13& b, uint32_t tr, uint32_t voff0, uint64_t sb,
+  auto compute = [&](uint32_t q, uint32_t geo, const Set8Meta& m, const Buf13& b, uint32_t voff0, uint64_t sb,
                      auto issue) {
     static_assert(kV8Pieces == 13, "the position sequence below");
     const uint32_t zo = w_zo(geo), P = w_P(geo), front = w_r(geo) + 4u;
@@ -525,6 +519,28 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
       return x;
     };
     Chains c{0u, 0u, 0u, 0u, 0u};
+    // The gate's trailer, from the registers of the last two lines (no load of its own): it starts
+    // at u = zo - 128 (P - 1) in line P - 1 (-3 .. 124; u < 0 only when it starts in the last word of
+    // line P - 2), in line words a0 = floor(u / 4) and a1 = a0 + 1, which lanes a >> 2 of the group
+    // hold as component a & 3: each lane picks the group's component and ds_bpermute gathers them.
+    const int u = (int)zo - 128 * (int)(P - 1u);
+    const uint32_t a1 = min((uint32_t)(u + 4) >> 2, 31u), a0 = max((uint32_t)(u + 4) >> 2, 1u) - 1u;
+    uint32_t tw_p = 0u, tw0 = 0u, tw1 = 0u;  // word 31 of line P - 2, words a0 and a1 of line P - 1
+    auto pick = [](const uint4& x, uint32_t k) {
+      const uint32_t lo = (k & 1u) ? x.y : x.x, hi = (k & 1u) ? x.w : x.z;
+      return (k & 2u) ? hi : lo;
+    };
+    auto trailer_words = [&](int s, const uint4& x) {
+      if constexpr (!SEAL) {
+        const uint32_t gb = L.lane & ~7u;
+        if (s == 11) {
+          tw_p = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + 7u) * 4u), (int)x.w);
+        } else if (s == 12) {
+          tw0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + (a0 >> 2)) * 4u), (int)pick(x, a0 & 3u));
+          tw1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + (a1 >> 2)) * 4u), (int)pick(x, a1 & 3u));
+        }
+      }
+    };
     auto masked_init = [&](uint4 x, int lim) {  // from zero chains: words past the end stay zero
       const uint4 d = end_masked(L.lds, x, lim);
       c = Chains{d.x, d.y, d.z, d.w, 0u};
@@ -532,6 +548,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     auto entry = [&](int s) {
       for (int k = 1; k < s; k++) issue(k);  // (slots this set does not use)
       const uint4 x = xin(s);
+      trailer_words(s, x);
       if (s == 12)
         masked_init(x, lim12);
       else if (s == 11 && !m.penult_data)
@@ -542,6 +559,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     };
     auto stepk = [&](int s) {
       const uint4 x = xin(s);
+      trailer_words(s, x);
       if (s == 12)
         chain4_masked(L, c, x, lim12);
       else if (s == 11 && !m.penult_data)
@@ -575,6 +593,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     }
     const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
     const uint32_t crc = ~unshift(group_lin8_rot(L, c, e), t);
+    const uint32_t tr = __builtin_amdgcn_alignbyte(tw1, u < 0 ? tw_p : tw0, (uint32_t)u & 3u);
     const uint32_t ok = (!SEAL && w_len(geo) >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     if (SEAL && L.col == 0u) {  // BE32 trailer: one (unaligned) dword store per frame
       // (non-temporal trailer stores measured slower: 1.912 against 1.874 ms)
@@ -649,14 +668,13 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // the registers S has just consumed; records one set ahead of their geometry ----
   Buf13 B;
   Rec O;  // record of set QO
-  uint32_t QO, QG, GE, VO, TR;  // QG: the set being computed (its geometry GE, VO, SB, M, trailer TR)
+  uint32_t QO, QG, GE, VO;  // QG: the set being computed (its geometry GE, VO, SB, M)
   uint64_t SB;
   Set8Meta M;
   {  // prologue: the first set's geometry and loads, the second set's record
     QG = next_q();
     const Rec r0 = load_rec(QG);
     GE = geometry(QG, r0, VO, M, SB);
-    TR = load_tr(VO, GE, SB);  // (the loop's order: the trailer, then the slots)
 #pragma unroll
     for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, B);
     QO = next_q();
@@ -674,19 +692,18 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
 
   // (a wave's sets are valid up to its first kNoSet)
   while (QG != kNoSet) {
-    // the next set: geometry from its record, its trailer; the record after it
+    // the next set: geometry from its record; the record after it
     uint32_t VN;
     uint64_t SBN;
     Set8Meta MN;
     const uint32_t QN = QO;
     const uint32_t GN = geometry(QN, O, VN, MN, SBN);
-    const uint32_t TRN = load_tr(VN, GN, SBN);
     QO = next_q();
     O = load_rec(QO);
     __builtin_amdgcn_sched_barrier(0);
     auto issue = [&](int k) { load_slot(k, VN, GN, SBN, B); };
     if (!M.slow) {
-      compute(QG, GE, M, B, TR, VO, SB, issue);
+      compute(QG, GE, M, B, VO, SB, issue);
     } else {
 #pragma unroll
       for (int k = 0; k < kV8Pieces; k++) issue(k);
@@ -698,7 +715,6 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     VO = VN;
     SB = SBN;
     M = MN;
-    TR = TRN;
   }
 }
 
