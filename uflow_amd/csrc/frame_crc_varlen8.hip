@@ -439,7 +439,12 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // before G and slots before a frame's line 1 are out of range (zeros, no request).  Slot k of a set
   // (k = 0: line 0; k >= 1: line k - 13 + P, out of range before line 1) is issued one at a time, as
   // the current set frees the slot's registers.
-  auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b) {
+  // dep (DEP): the chain words of the position that has just consumed slot k: the load is issued
+  // after them, so that it can take the slot's own registers (otherwise the scheduler issues it
+  // while the position's last XORs still read the slot, the load goes into other registers, and each
+  // straight copy of the positions ends with a different register assignment, moved back at the
+  // loop's merge behind a vmcnt(1) wait)
+  auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b, const Chains* dep) {
     const uint32_t P = w_P(geo), front = w_r(geo) + 4u;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
     if (k == 0) {
@@ -454,7 +459,10 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     uint32_t vo = (uint32_t)k + P >= 14u ? base : kV8Oob;
     // (opaque to the optimizer: otherwise it pushes the slot's constant 128 k through the select, one
     // more add and one more register per slot, instead of the load's immediate offset)
-    asm("" : "+v"(vo));
+    if (dep)
+      asm("" : "+v"(vo) : "v"(dep->v0), "v"(dep->v1), "v"(dep->v2), "v"(dep->v3));
+    else
+      asm("" : "+v"(vo));
     u32x4 v;
     if (k == kV8Pieces - 1)
       v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxShared);
@@ -555,7 +563,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
         masked_init(x, lim11);
       else
         c = Chains{x.x, x.y, x.z, x.w, 0u};
-      if (s > 0) issue(s);
+      if (s > 0) issue(s, &c);
     };
     auto stepk = [&](int s) {
       const uint4 x = xin(s);
@@ -566,7 +574,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
         chain4_masked(L, c, x, lim11);
       else
         chain4(L, c, x);
-      issue(s);
+      issue(s, &c);
     };
     // one straight copy of the positions per entry point (no merges inside: the loads the positions
     // issue keep one order on every path, so their waits stay counted)
@@ -676,7 +684,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     const Rec r0 = load_rec(QG);
     GE = geometry(QG, r0, VO, M, SB);
 #pragma unroll
-    for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, B);
+    for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, B, nullptr);
     QO = next_q();
     O = load_rec(QO);
   }
@@ -701,7 +709,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     QO = next_q();
     O = load_rec(QO);
     __builtin_amdgcn_sched_barrier(0);
-    auto issue = [&](int k) { load_slot(k, VN, GN, SBN, B); };
+    auto issue = [&](int k, const Chains* dep = nullptr) { load_slot(k, VN, GN, SBN, B, dep); };
     if (!M.slow) {
       compute(QG, GE, M, B, VO, SB, issue);
     } else {
