@@ -23,7 +23,7 @@
 //     switch on its longest frame); line 0 (slot 0, loaded apart for its cache policy) goes in at
 //     position 13 - P.  Only positions 11 and 12 can need masked steps.
 //   * One set buffer per wave, software-pipelined: each slot of the next set is issued as soon as the
-//     current set has consumed that slot's registers (126 VGPRs: 16 waves per CU).  The straight copy
+//     current set has consumed that slot's registers (128 VGPRs: 16 waves per CU).  The straight copy
 //     per entry point keeps the order of those loads the same on every path, so the compiler's load
 //     waits stay counted (with one shared sequence it waited for every load at each entry point).
 //   * Sets come from runs of 64 frames sorted by line count in the wave that takes them (four one-bit
@@ -236,7 +236,7 @@ struct Buf13 {
 
 }  // namespace
 
-// One workgroup of kV8Waves waves per CU (126 VGPRs: 4 waves per SIMD), one set buffer per wave,
+// One workgroup of kV8Waves waves per CU (128 VGPRs: 4 waves per SIMD), one set buffer per wave,
 // software-pipelined: the next set's slots are issued into the registers the current set has just
 // consumed.  p.offsets = the CSR offsets (n + 1) or, with PAIRS, the (start, end) pairs (p.frame_len =
 // the buffer length).  Each run of 64 frames is ordered by line count in the wave that takes it,
