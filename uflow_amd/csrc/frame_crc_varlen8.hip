@@ -227,11 +227,9 @@ struct Set8Meta {
 };
 
 // A set's loads, right-aligned: slot 0 = line 0, slot s >= 1 = line s - 13 + P (its last line P - 1 in
-// slot 12; slots that would hold line 0 or a line before it are out of range, zeros); tr = the
-// trailer (4 bytes at zo).
+// slot 12; slots that would hold line 0 or a line before it are out of range, zeros).
 struct Buf13 {
   uint4 x[kV8Pieces];
-  uint32_t tr = 0;
 };
 
 }  // namespace
