@@ -374,6 +374,8 @@ def main():
     if sharded:
         with _StdoutToStderr():
             dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm: barriers and the timing max
+            # A host-side group for waits that must not put RCCL kernels on the GPU (n1_sharded_ref)
+            host_group = dist.new_group(backend="gloo") if world > 1 else None
 
     from uflow_amd import synth
     from uflow_amd.batch import FrameCrcEngine
@@ -538,13 +540,17 @@ def main():
         ok = ok and exact and all_local_ok
 
     # N > 1: config 4's batch gated by rank 0's GPU alone (the N = 1 point of the same workload, no
-    # gather), after the timed region, every other rank waiting at the barrier: the driver's 1 -> N curve
-    # then separates the gate's scaling from the gather's cost and from the batch size.
+    # gather), after the timed region: the driver's 1 -> N curve then separates the gate's scaling from
+    # the gather's cost and from the batch size.  The other ranks wait on the host (a gloo barrier), not
+    # on an RCCL barrier: with --one-device the RCCL barrier's kernels would share rank 0's GPU while it
+    # times the reference (2545 GiB/s there against 5940 alone).
     n1_ref = None
     if sharded and world > 1 and not a.no_n1_ref:
+        torch.cuda.synchronize(dev)
+        dist.barrier(group=host_group)  # every rank idle on the GPU before rank 0 starts timing
         if rank == 0:
             n1_ref = n1_sharded_reference(eng, total, L, seed, a.flip_every, dev)
-        dist.barrier()
+        dist.barrier(group=host_group)
 
     result = None
     if rank == 0:
@@ -581,7 +587,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8, 4224> (ufc_crc_batch_fixed"
+                "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 2, 8, 4224> (ufc_crc_batch_fixed"
                           + (", per chunk of ufc_crc_sharded" if sharded else "") + ")",
                 "kernel_avg_ms": round(kern_ms, 4),
                 "kernel_median_ms": round(float(np.median(kern_all)), 4),

@@ -78,6 +78,9 @@ int ufc_frame_seal(uint8_t* frame, size_t len);
 typedef struct ufc_ctx ufc_ctx;
 int ufc_device_count(void);
 int ufc_ctx_create(ufc_ctx** out, int device);
+/* UFC_OK; UFC_ERR_COMM when a communicator created on this context stalled (ufc_comm_set_timeout):
+ * its RCCL all-reduce stays pending on the device, so the context's device memory and streams are
+ * left to process exit (freeing them would wait for the device for ever); the handle is freed. */
 int ufc_ctx_destroy(ufc_ctx* ctx);
 /* Device scratch is kept per (context, stream) and grows only (batch parse: 14 B per frame + 2 B per
  * header slot, min(64 n, items_cap) slots; fixed seal without d_crc_out: 4 B per frame; asynchronous
@@ -107,9 +110,9 @@ int ufc_ctx_last_hip_error(const ufc_ctx* ctx);
 #define UFC_VARLEN_STREAM 7      /*   (removed) the byte-balanced stream kernel */
 #define UFC_OPT_GENERIC_JC 2     /* 0 = auto, else 1..6: blocks per pipelined part of the generic kernel */
 #define UFC_OPT_SEAL_KERNEL 3    /* fixed-stride seals: */
-#define UFC_SEAL_TWO_PASS 0      /*   validate kernel's CRC words, then a non-temporal trailer pass (the round-3 default) */
-#define UFC_SEAL_INLINE 1        /*   the CRC kernel writes each workgroup's trailers after its reads (the default
-                                  *   since round 4: ufc_ctx_create sets it) */
+#define UFC_SEAL_INLINE 0        /*   the CRC kernel writes each workgroup's trailers after its reads (default; the
+                                  *   numbers of round 4's header, kept: ufc_ctx_create sets the default explicitly) */
+#define UFC_SEAL_TWO_PASS 1      /*   validate kernel's CRC words, then a non-temporal trailer pass (the round-3 default) */
 #define UFC_OPT_COUNT_ 4
 int ufc_ctx_set_option(ufc_ctx* ctx, int option, int value);
 int ufc_ctx_get_option(const ufc_ctx* ctx, int option);
@@ -247,7 +250,9 @@ int ufc_comm_last_error(const ufc_comm* comm);
  * deadline (ufc_comm_set_timeout; crashed, or calling something else) fails the call with
  * UFC_ERR_COMM without aborting anything (ncclCommAbort measured not to return while the peer has not
  * joined, on the socket transport): the communicator is then stalled, every later call returns
- * UFC_ERR_COMM, and the caller should end the process with an error.  A failure that only this rank
+ * UFC_ERR_COMM, and the caller should end the process with an error.  The agreement takes two rounds
+ * (status, then commit), so a peer that makes the call after the deadline has passed on another rank
+ * fails with UFC_ERR_COMM at its own deadline too, instead of queueing a gather nobody answers.  A failure that only this rank
  * sees after the gather has begun (a HIP launch error) aborts the communicator (ncclCommAbort) and
  * marks it unusable (later calls return UFC_ERR_COMM): the peers' transfers then fail or stall, and
  * the caller must tear down every rank's communicator. */

@@ -15,6 +15,14 @@ never calls ufc_crc_sharded; rank 0 calls it with a 3-s deadline (ufc_comm_set_t
 UFC_ERR_COMM within the deadline instead of hanging, then UFC_ERR_COMM at once from the stalled
 communicator, prints what it saw and exits with status 3 (os._exit: the pending all-reduce is left to
 process exit); rank 1 leaves once rank 0 has answered.
+
+--late-peer (world 2): a peer that makes the call only after the other rank's deadline has
+passed.  Rank 0 calls with a 3-s deadline and fails (UFC_ERR_COMM, stalled); only then does rank 1 call,
+with a 3-s deadline of its own.  Its status round completes against rank 0's pending all-reduce, but the
+commit round finds no partner, so rank 1 must fail with UFC_ERR_COMM at its deadline too, not go on to a
+gather nobody answers.  Each rank then closes its communicator and its context (ufc_ctx_destroy must
+return, not wait for the pending all-reduce) and reports how long that took; rank 0 stays alive until
+rank 1 is done and prints both ranks' results.
 """
 import json
 import os
@@ -76,6 +84,59 @@ def peer_timeout():
     with open(flag, "w") as f:
         f.write("done")
     os._exit(3 if codes[0] == UFC_ERR_COMM else 4)
+
+
+def late_peer():
+    from uflow_amd._native import UFC_ERR_COMM, NativeError
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", device_id=dev)
+    eng = FrameCrcEngine(0)
+    idt = torch.zeros(128, dtype=torch.uint8, device=dev)
+    if rank == 0:
+        idt.copy_(torch.frombuffer(bytearray(comm_id_create()), dtype=torch.uint8))
+    dist.broadcast(idt, src=0)
+    gate = ShardedGate(eng, world, rank, bytes(idt.cpu().numpy()))
+    torch.cuda.synchronize()
+    tag = os.environ["MASTER_PORT"]
+    flag0 = os.path.join("/tmp", "ufc_late_peer_%s.r0" % tag)
+    flag1 = os.path.join("/tmp", "ufc_late_peer_%s.r1" % tag)
+    total, L = 100_000, 64
+    b = shard_bounds_fixed(total, world)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    frames = synth.fixed_frames(hi - lo, L, synth.SEED_CONFIG4, device=dev)
+    crc = torch.full((total if rank == 0 else hi - lo,), -1, dtype=torch.int32, device=dev)
+    gate.set_timeout(3000)
+    if rank == 1:  # late: only after rank 0 has given up
+        t0 = time.monotonic()
+        while not os.path.exists(flag0) and time.monotonic() - t0 < 90:
+            time.sleep(0.05)
+    t0 = time.monotonic()
+    try:
+        gate.crc_sharded(frames, L, total, crc, None, root=0)
+        code = 0
+    except NativeError as e:
+        code = e.code
+    t_call = round(time.monotonic() - t0, 3)
+    t0 = time.monotonic()
+    gate.close()
+    eng.close()  # must return although an all-reduce is pending on the device
+    t_close = round(time.monotonic() - t0, 3)
+    mine = {"rank": rank, "code": code, "t_call": t_call, "t_close": t_close}
+    if rank == 0:
+        with open(flag0, "w") as f:
+            f.write(json.dumps(mine))
+        t0 = time.monotonic()
+        while not os.path.exists(flag1) and time.monotonic() - t0 < 90:
+            time.sleep(0.05)
+        time.sleep(0.2)
+        other = json.loads(open(flag1).read()) if os.path.exists(flag1) else None
+        print(json.dumps({"late_peer": [mine, other], "UFC_ERR_COMM": UFC_ERR_COMM}), flush=True)
+        os._exit(0)
+    with open(flag1 + ".tmp", "w") as f:
+        f.write(json.dumps(mine))
+    os.replace(flag1 + ".tmp", flag1)
+    os._exit(0)
 
 
 def main():
@@ -176,5 +237,7 @@ def main():
 if __name__ == "__main__":
     if "--peer-timeout" in sys.argv:
         peer_timeout()
+    elif "--late-peer" in sys.argv:
+        late_peer()
     else:
         main()

@@ -273,3 +273,46 @@ def test_datagram_is_valid_vs_oracle():
         dg = dict(ok, **change)
         assert C.datagram_is_valid(dg) == want, change
         assert F.datagram_is_valid(F.Datagram(**dg)) == want, change
+
+
+def test_parse_expect_records_vs_host_parse():
+    """tests/parse_expect.py (the oracle-built records the full-size GPU parse tests compare with) ==
+    the native host parse, on every frame kind, damaged frames, and a tiled batch with flipped frames."""
+    import parse_expect
+    rng = random.Random(606)
+    frames = []
+    for i in range(900):
+        r = i % 6
+        if r == 0:
+            frames.append(C.frame_write(C.random_data_frame(rng)))
+        elif r == 1:
+            frames.append(C.frame_write(C.random_ack_frame(rng, 30)))
+        elif r == 2:
+            frames.append(C.frame_write(C.random_sync_frame(rng)))
+        elif r == 3:
+            frames.append(C.frame_write(C.receive_side_data_frame(rng)))
+        elif r == 4:
+            frames.extend(_mutants(rng, 1))
+        else:
+            frames.append(C.frame_write(C.reference_test_frames()[i % 12][1]))
+    data, offsets = _batch(frames)
+    exp_infos, exp_items = parse_expect.oracle_records(frames)
+    infos, items = F.parse_batch_host(data, offsets, None, nthreads=4)
+    parse_expect.compare(infos, items, exp_infos, exp_items)
+    assert items.size == exp_items.size
+    # tiled, with flipped frames (the full-size tests' expansion)
+    reps = 7
+    n = len(frames) * reps
+    tile = np.arange(n) % len(frames)
+    lens = np.diff(offsets.astype(np.int64))
+    big = np.tile(data, reps)
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum(np.tile(lens, reps))
+    flip = np.array([i for i in range(0, n, 13) if lens[tile[i]] >= 5 and exp_infos["crc_ok"][tile[i]]])
+    big[offs[flip].astype(np.int64) + lens[tile[flip]] // 2] ^= 0x10
+    dead = np.zeros(n, dtype=bool)
+    dead[flip] = True
+    t_infos, t_items = parse_expect.tile_records(exp_infos, exp_items, tile, dead)
+    infos, items = F.parse_batch_host(big, offs, None, nthreads=4)
+    parse_expect.compare(infos, items, t_infos, t_items)
+    assert items.size == t_items.size

@@ -209,10 +209,12 @@ def test_parse_bench_workload_full(engine, mtu):
     """The parse workloads tools/bench_configs.py times (1M uflow frames: data frames with
     micro/small/large datagrams, receive-side data frames and ack frames, 600 distinct frames from the
     codec oracle tiled; 1.41 GB, or 0.60 GB with every frame <= MAX_FRAME_SIZE), with one bit flipped in
-    every 997th frame: the GPU gate + GPU parse vs the native host parse with its own host gate
-    (ufc_parse_batch_host, pinned to the codec oracle by the CPU suite), every info and every item
-    compared."""
-    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host
+    every 997th frame: the GPU gate + GPU parse against the codec oracle.  The 600
+    distinct frames are decoded by oracle/codec.py frame_read and laid out as the C ABI's records; the
+    1M frames' expected infos and items are those records expanded over the tiling (a flipped frame:
+    not ok, no items), and every info and every item of the GPU output is compared with them."""
+    import parse_expect
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE
     n = 1_000_000
     base = _parse_workload_base(mtu)
     lens = np.array([len(base[i % 600]) for i in range(n)], dtype=np.int64)
@@ -230,13 +232,14 @@ def test_parse_bench_workload_full(engine, mtu):
     k = int(used.cpu()[0])
     got_infos = _host(infos).view(FRAME_INFO_DTYPE).reshape(-1)
     got_items = _host(items[:k]).view(ITEM_DTYPE).reshape(-1)
-    ref_infos, ref_items = parse_batch_host(data, offsets.astype(np.uint64), None, nthreads=THREADS)
+    b_infos, b_items = parse_expect.oracle_records(base)
+    assert b_infos["ok"].all()
+    dead = np.zeros(n, dtype=bool)
+    dead[flipped] = True
+    exp_infos, exp_items = parse_expect.tile_records(b_infos, b_items, np.arange(n) % 600, dead)
     assert int(got_infos["crc_ok"].sum()) == n - flipped.size
-    assert k == ref_items.size and k > (11_000_000 if mtu else 14_000_000), k
-    bad = np.nonzero((got_infos.view(np.uint8).reshape(n, -1) != ref_infos.view(np.uint8).reshape(n, -1)).any(1))[0]
-    assert bad.size == 0, f"{bad.size} frame infos differ, first frames {bad[:8]}"
-    bad = np.nonzero((got_items.view(np.uint8).reshape(k, -1) != ref_items.view(np.uint8).reshape(k, -1)).any(1))[0]
-    assert bad.size == 0, f"{bad.size} items differ, first items {bad[:8]}"
+    assert k == exp_items.size and k > (11_000_000 if mtu else 14_000_000), k
+    parse_expect.compare(got_infos, got_items, exp_infos, exp_items)
 
 
 def test_parse_datagram_validity_flags(engine):
@@ -305,10 +308,13 @@ def test_varlen_claimed_runs_with_slow_sets(engine):
 
 def test_parse_large_batch(engine):
     """A 4.32M-frame parse (the codec test batch tiled 7200 times, 16875 workgroups, 1.3 GB): every
-    frame's info and the item count against the native host parse."""
+    frame's info and every item against the codec oracle (the 600 distinct frames decoded by
+    oracle/codec.py frame_read, expanded over the tiling), and against the native host parse gating
+    on its own (valid = None: nothing of the GPU's output goes into the reference)."""
+    import parse_expect
     from test_gpu_parity import _codec_batch
-    from uflow_amd.frame import FRAME_INFO_DTYPE, parse_batch_host
-    _, data, offsets = _codec_batch(10, 600)
+    from uflow_amd.frame import FRAME_INFO_DTYPE, ITEM_DTYPE, parse_batch_host
+    frames, data, offsets = _codec_batch(10, 600)
     reps = 7200
     lens = np.diff(offsets)
     big = np.tile(data, reps)
@@ -320,8 +326,14 @@ def test_parse_large_batch(engine):
     _, valid = engine.crc_varlen(d, o)
     infos, items, used = engine.parse_varlen(d, o, valid)
     torch.cuda.synchronize()
+    k = int(used.cpu()[0])
     got = _host(infos).view(FRAME_INFO_DTYPE).reshape(-1)
-    ref, ref_items = parse_batch_host(big, offs.astype(np.uint64), _host(valid), nthreads=THREADS)
+    got_items = _host(items[:k]).view(ITEM_DTYPE).reshape(-1)
+    b_infos, b_items = parse_expect.oracle_records(frames)
+    exp_infos, exp_items = parse_expect.tile_records(b_infos, b_items, np.arange(n) % 600, np.zeros(n, dtype=bool))
+    assert k == exp_items.size
+    parse_expect.compare(got, got_items, exp_infos, exp_items)
+    ref, ref_items = parse_batch_host(big, offs.astype(np.uint64), None, nthreads=THREADS)
     bad = np.nonzero((got.view(np.uint8).reshape(n, -1) != ref.view(np.uint8).reshape(n, -1)).any(1))[0]
-    assert bad.size == 0, f"{bad.size} frame infos differ, first frames {bad[:8]}"
-    assert int(used.cpu()[0]) == ref_items.size
+    assert bad.size == 0, f"{bad.size} frame infos differ from the host parse, first frames {bad[:8]}"
+    assert k == ref_items.size

@@ -177,3 +177,22 @@ def test_sharded_peer_timeout():
     assert 2.5 <= t0 <= 30.0, j   # the deadline, not a hang
     assert t1 - t0 < 1.0, j       # a stalled communicator fails at once
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+
+
+def test_sharded_late_peer():
+    """A peer that calls only after the other rank's deadline has passed: rank 0 fails with
+    UFC_ERR_COMM at its 3-s deadline; rank 1 then calls and must fail with UFC_ERR_COMM at its own 3-s
+    deadline (the commit round finds no partner) instead of queueing a gather that hangs.  Both ranks
+    then close the communicator and the context: ufc_ctx_destroy returns at once although an
+    all-reduce stays pending on the device (tests/gpu_shard_worker.py --late-peer)."""
+    p = _run_worker(2, ["--late-peer"], 150)
+    objs = re.findall(r"\{\"late_peer\".*\}", p.stdout)
+    assert len(objs) == 1, (p.stdout[-2000:], p.stderr[-2000:])
+    j = json.loads(objs[0])
+    r0, r1 = j["late_peer"]
+    assert r1 is not None, j
+    for r in (r0, r1):
+        assert r["code"] == j["UFC_ERR_COMM"], j
+        assert 2.5 <= r["t_call"] <= 30.0, j  # the deadline, not a hang, and not an early success
+        assert r["t_close"] < 5.0, j          # teardown does not wait for the pending all-reduce
+    assert p.returncode == 0, (p.returncode, p.stderr[-2000:])

@@ -1,4 +1,4 @@
-"""Build an experiment variant of libuflowcrc.so into abl/<name>.so: the product sources copied to a
+"""Build an experiment variant of libuflowcrc.so into var/<name>.so: the product sources copied to a
 scratch tree, `file:old=>new` substitutions applied (each must match), compiled with the product's
 flags.  A/B measurement only (tools/ab_inproc.py); the product library is never touched.
 `file@path` replaces a source file of the copy with another file (e.g. an earlier round's, from git show);
@@ -32,23 +32,26 @@ def main():
         s = open(p).read()
         assert old in s, f"{fn}: no match for {old!r}"
         open(p, "w").write(s.replace(old, new))
-    sources, flags, _ = _build._native_identity()
+    sources, flags, per_source, _ = _build._native_identity()
     flags = flags + os.environ.get("VARIANT_FLAGS", "").split()
-    for opt in os.environ.get("VARIANT_NO_MLLVM", "").split():
-        i = flags.index(opt)
-        assert flags[i - 1] == "-mllvm", opt
-        del flags[i - 1:i + 1]
+    drop = os.environ.get("VARIANT_NO_MLLVM", "").split()
     objs = []
     jobs = []
     for src in sources:
         obj = os.path.join(d, src + ".o")
         objs.append(obj)
-        jobs.append(flags + ["-c", os.path.join(d, "uflow_amd", "csrc", src), "-o", obj])
+        f = flags + per_source.get(src, [])
+        for opt in drop:
+            if opt in f:
+                i = f.index(opt)
+                assert f[i - 1] == "-mllvm", opt
+                del f[i - 1:i + 1]
+        jobs.append(f + ["-c", os.path.join(d, "uflow_amd", "csrc", src), "-o", obj])
     with ThreadPoolExecutor(8) as ex:
         rcs = list(ex.map(lambda c: subprocess.run(c).returncode, jobs))
     assert not any(rcs), rcs
-    os.makedirs(os.path.join(REPO, "abl"), exist_ok=True)
-    out = os.path.join(REPO, "abl", name + ".so")
+    os.makedirs(os.path.join(REPO, "var"), exist_ok=True)
+    out = os.path.join(REPO, "var", name + ".so")
     subprocess.run([_build.HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out] + objs + ["-ldl"], check=True)
     shutil.rmtree(d)
     print(out)

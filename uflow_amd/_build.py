@@ -65,14 +65,22 @@ def _native_identity(defines=()):
     deps += [os.path.join(REPO_DIR, "include", h) for h in ("uflow_frame_crc.h", "uflow_frame_codec.h")]
     # No atomic optimizer: the lean kernel's single-lane claim atomics must stay plain
     # global_atomic_add (the optimizer reads the result back at once, forcing a vmcnt(0) wait).
-    # Uniform branches left unstructured: the variable-length kernel's set-level branches (a switch on
-    # the set's line count, masked or plain steps) otherwise get "Flow" blocks that copy the chain
-    # registers at every merge (1.585 against 1.484 ms on config 3, profiles/EXPERIMENTS.md).
     flags = [HIPCC, "-O3", "--offload-arch=gfx950", "-fPIC", "-std=c++17", "-Wall",
-             "-mllvm", "-amdgpu-atomic-optimizer-strategy=None",
-             "-mllvm", "-structurizecfg-skip-uniform-regions=true"]
+             "-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
     flags += ["-D" + d for d in defines]
-    return sources, flags, _digest(deps + [os.path.abspath(__file__)], flags[1:])
+    per_source = {s: list(UNSTRUCTURED_FLAGS) for s in UNSTRUCTURED_SOURCES}
+    extra = [f"{s}:{' '.join(per_source[s])}" for s in sorted(per_source)]
+    return sources, flags, per_source, _digest(deps + [os.path.abspath(__file__)], flags[1:] + extra)
+
+
+# Uniform branches left unstructured, per source: the variable-length kernel's set-level branches (a
+# switch on the set's line count, masked or plain steps) otherwise get "Flow" blocks that copy the
+# chain registers at every merge (1.585 against 1.484 ms on config 3, profiles/EXPERIMENTS.md).  The
+# fixed kernels of frame_crc.hip were measured with it (round 5: the bench kernel's 224.8 us), so it
+# stays there too; the parse (frame_parse.hip) and the probe build without it (a non-default
+# option is applied only where it was measured).
+UNSTRUCTURED_FLAGS = ("-mllvm", "-structurizecfg-skip-uniform-regions=true")
+UNSTRUCTURED_SOURCES = ("frame_crc_varlen8.hip", "frame_crc.hip")
 
 
 def build_native(force=False, verbose=False, out=None, defines=()):
@@ -82,7 +90,7 @@ def build_native(force=False, verbose=False, out=None, defines=()):
     Rebuilds when the sha256 of the sources, headers, flags and this file differs from the one
     recorded beside the library (<lib>.sha256), not by file times: a library copied to another
     machine (the GPU box) with its stamp is rebuilt there only if it does not match the source."""
-    sources, flags, digest = _native_identity(defines)
+    sources, flags, per_source, digest = _native_identity(defines)
     target = out or LIB_PATH
     if not force and _stamp_ok(target, digest):
         return target
@@ -93,7 +101,7 @@ def build_native(force=False, verbose=False, out=None, defines=()):
     for src in sources:
         obj = os.path.join(objdir, src + ".o")
         objs.append(obj)
-        jobs.append(flags + ["-c", os.path.join(CSRC, src), "-o", obj])
+        jobs.append(flags + per_source.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj])
     from concurrent.futures import ThreadPoolExecutor
 
     def run(cmd):

@@ -10,9 +10,10 @@ import os
 
 from ._build import LIB_PATH as _DEFAULT_LIB
 
-# UFC_LIB overrides the library path (A/B measurement against another build; the product loads the
-# in-tree .so).
-LIB_PATH = os.environ.get("UFC_LIB", _DEFAULT_LIB)
+# Measurement tools only: with UFC_AB=1 set as well, UFC_LIB names another build of the library to
+# load (in-process A/B runs under tools/).  Without the guard the in-tree library is the one loaded,
+# whatever UFC_LIB says ("Test-only environment").
+LIB_PATH = os.environ["UFC_LIB"] if os.environ.get("UFC_AB") == "1" and os.environ.get("UFC_LIB") else _DEFAULT_LIB
 
 UFC_OK = 0
 UFC_ERR_INVALID_ARG = -1
@@ -30,7 +31,7 @@ UFC_OPT_FIXED_KERNEL, UFC_OPT_VARLEN_KERNEL, UFC_OPT_GENERIC_JC = 0, 1, 2
 UFC_FIXED_AUTO, UFC_FIXED_GENERIC, UFC_FIXED_CLAIM16 = 0, 1, 2
 UFC_VARLEN_AUTO, UFC_VARLEN_GENERIC, UFC_VARLEN_SORTED, UFC_VARLEN_BLOCKED8, UFC_VARLEN_CLAIM16 = 0, 1, 2, 3, 4
 UFC_VARLEN_BLOCKSTREAM, UFC_VARLEN_SORTED8, UFC_VARLEN_STREAM = 5, 6, 7
-UFC_OPT_SEAL_KERNEL, UFC_SEAL_INLINE, UFC_SEAL_TWO_PASS = 3, 1, 0
+UFC_OPT_SEAL_KERNEL, UFC_SEAL_INLINE, UFC_SEAL_TWO_PASS = 3, 0, 1
 
 # Every symbol the header declares, with its ctypes signature.
 _c_u8p = ctypes.POINTER(ctypes.c_uint8)

@@ -115,8 +115,6 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
   constexpr bool FREEZE = VARLEN || (MODE & kModeFreeze) != 0;  // blocks past J may occur in a part
   // Fixed-length frames without freeze: the host picks JC == J, so every set is one part.
   constexpr bool SINGLE = !VARLEN && (MODE & kModeFreeze) == 0;
-  constexpr bool NO_COMPUTE = (MODE & kModeAblateCompute) != 0;  // tuning builds only
-  constexpr bool NO_LOADS = (MODE & kModeAblateLoads) != 0;      // tuning builds only
   // Static LDS (all 160 KiB): its base is the constant 0, so a perm result IS the LDS address (a
   // dynamic-LDS base would cost one v_add per table lookup).
   __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
@@ -272,16 +270,7 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
   // step), compute C0 from `cur`, shift the cursors.  Loads are unconditional: a load behind a
   // branch makes the waitcnt pass assume it was skipped and wait for the whole prefetch.
   auto step = [&](ItemBuf<JC>& cur, ItemBuf<JC>& nxt2) -> bool {
-    if (NO_LOADS) {
-#pragma unroll
-      for (int j = 0; j < JC; j++) nxt2.x[j] = make_uint4(cur.x[j].y, cur.x[j].z, cur.x[j].w, cur.x[j].x ^ C2.part);
-    }
-    if (NO_COMPUTE) {
-      if (!NO_LOADS) load_cursor(C2, nxt2);
-#pragma unroll
-      for (int j = 0; j < JC; j++) c.v0 ^= cur.x[j].x ^ cur.x[j].y ^ cur.x[j].z ^ cur.x[j].w;
-      c.tr = c.v0;
-    } else {
+    {
       // The prefetch of C2 is spread over the compute of C0, one block load per block of compute,
       // pinned by sched_barrier: a wave that issued all its loads up front would stall at VMEM issue
       // behind the other waves' bursts instead of computing.
@@ -291,10 +280,8 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
       if (!p0) __builtin_assume(C0.part >= 1);
 #pragma unroll
       for (int j = 0; j < JC; j++) {
-        if (!NO_LOADS) {
-          const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
-          nxt2.x[j] = make_uint4(v.x, v.y, v.z, v.w);
-        }
+        const u32x4 v = __builtin_nontemporal_load(as_global<g_u32x4>(q + 256 * j));
+        nxt2.x[j] = make_uint4(v.x, v.y, v.z, v.w);
         __builtin_amdgcn_sched_barrier(0);
         if (p0)
           process_block<FREEZE>(L, C0.d, j, cur.x[j], c);
@@ -348,8 +335,6 @@ __global__ __launch_bounds__(1024) void frame_crc_kernel(const KernelParams p) {
 // hoisted, set addresses are scalar, results gather with one select per set.  DEPTH sets are in
 // flight per wave (DEPTH-1 prefetched while one is computed); the first prefetches are issued
 // before the LDS tables are staged so that HBM is busy from the first cycle.
-// ABL (tuning builds only): kLeanAblLoads = loads + XOR fold, no CRC; kLeanAblCompute = CRC of
-// the prologue's registers, no loads in the loop.  Their results are meaningless.
 // ---------------------------------------------------------------------------------------------
 
 // Per-workgroup claim counters of the dynamic schedule (kCtrWordsPerBlock words per workgroup,
@@ -366,13 +351,10 @@ constexpr int lean_loadv(int skip, int first, int mid, int last) { return skip |
 // Product (round 4): default policy for block 0, non-temporal for the rest: 0.2277-0.2289 against
 // 0.2372-0.2383 ms per 1M x 1500 B (in-process A/B, identical results; profiles/EXPERIMENTS.md).
 constexpr int kLoadvProduct = lean_loadv(0, 0, kFixAuxNT, kFixAuxNT);
-template <int J, bool SEAL, int DEPTH, int ABL_, int SCHED, int WAVES, int LOADV = kLoadvProduct>
+template <int J, bool SEAL, int DEPTH, int SCHED, int WAVES, int LOADV = kLoadvProduct>
 __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const KernelParams p) {
   static_assert(DEPTH >= 1 && DEPTH <= 3, "pipeline depth (4 spills at J = 6)");
   static_assert(DEPTH != 1 || SCHED != kSchedClaim, "depth 1: static schedules only");
-  // Tuning ablation 5: loads only without the per-set finish.
-  constexpr bool NO_FINISH = ABL_ == 5;
-  constexpr int ABL = NO_FINISH ? kLeanAblLoads : ABL_;
   constexpr bool DYN = SCHED == kSchedClaim;        // claimed sets (per-workgroup counter)
   constexpr bool ILV = SCHED == kSchedInterleave;   // static: wave i takes lo + i + k * WAVES
   constexpr uint32_t kInc = ILV ? (uint32_t)WAVES : 1u;  // step of a static sequence
@@ -500,7 +482,7 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   // vmcnt(0) so that no store stays pending into the loop; the static schedules never overflow
   // inside the loop (host chunking), so their loop has no store.
   auto finish = [&](uint32_t q, const Chains& c, bool may_overflow) {
-    const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
+    const uint32_t crc = ~group_lin(L, c);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
     const uint32_t ok = (len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     acc_crc = (L.col == (int)t) ? crc : acc_crc;
@@ -526,20 +508,11 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
   // Frame-set processing from a loaded item (J blocks), block by block.
   auto compute_block = [&](uint32_t q, int j, uint4 x, Chains& c) {
     {
-      if (ABL == kLeanAblCompute && j == 0) {  // not loop-invariant
-        x.x ^= q; x.y ^= q; x.z ^= q; x.w ^= q;
-      }
       if (j == J - 1) {
         c.tr = x.w;
         x.w &= tmask;
       }
-      if (ABL == kLeanAblLoads) {
-        if (j == 0) {
-          c.v0 = x.x; c.v1 = x.y; c.v2 = x.z; c.v3 = x.w;
-        } else {
-          c.v0 ^= x.x; c.v1 ^= x.y; c.v2 ^= x.z; c.v3 ^= x.w;
-        }
-      } else if (j == 0) {
+      if (j == 0) {
         c.v0 = (x.x & dm[0]) | pre[0];
         c.v1 = (x.y & dm[1]) | pre[1];
         c.v2 = (x.z & dm[2]) | pre[2];
@@ -688,16 +661,13 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
     } else {
       q_load = (DEPTH == 3) ? q_nx2 : q_nx1;
     }
-    if (ABL != kLeanAblCompute) load(q_load, fill);
+    load(q_load, fill);
     // Issue the prefetch before the first wait on `cur`: a wave whose data is late must not
     // also hold back its next requests.
     __builtin_amdgcn_sched_barrier(0);
     if (q_cur < q_end) {
       compute(q_cur, cur, c);
-      if (NO_FINISH)
-        acc_crc ^= c.v0 ^ c.v1 ^ c.v2 ^ c.v3;
-      else
-        finish(q_cur, c, DYN);
+      finish(q_cur, c, DYN);
     }
     __builtin_amdgcn_sched_barrier(0);
     if (DEPTH == 3) {
@@ -740,16 +710,12 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
       step(C, B, cZ, cX);
     }
   }
-  if (NO_FINISH) {  // keep the folded loads alive (tuning ablation)
-    if (p.crc_out) p.crc_out[blockIdx.x * blockDim.x + threadIdx.x] = acc_crc;
-    return;
-  }
   // The partial last set (grid's last wave; before any LDS reuse below), results stored directly.
   if (tail && blockIdx.x == gridDim.x - 1 && wid == wpb - 1) {
     ItemBuf<J> T;
     load_tail(T);
     compute(nfull, T, c);
-    const uint32_t crc = (ABL == kLeanAblLoads) ? c.v0 ^ c.v1 ^ c.v2 ^ c.v3 : ~group_lin(L, c);
+    const uint32_t crc = ~group_lin(L, c);
     const uint32_t tr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c.tr, 0x15F, 0xF, 0xF, false);
     const uint32_t ok = (len >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     const uint64_t f = (uint64_t)nfull * 4 + (uint64_t)L.grp;
@@ -837,18 +803,18 @@ __global__ __launch_bounds__(WAVES * 64) void frame_crc_fixed_kernel(const Kerne
 // section 5.1).  The claimed schedule at 16 waves / depth 3 (the round-1 default) is instantiated
 // only in tuning builds (fixed_kernel_symbol, UFC_FIXED_CLAIM16).
 #define UFC_INST_FIXED(J)                                                                                  \
-  template __global__ void frame_crc_fixed_kernel<J, false, 2, 0, kSchedInterleave, 8>(const KernelParams); \
-  template __global__ void frame_crc_fixed_kernel<J, true, 2, 0, kSchedInterleave, 8>(const KernelParams);
+  template __global__ void frame_crc_fixed_kernel<J, false, 2, kSchedInterleave, 8>(const KernelParams); \
+  template __global__ void frame_crc_fixed_kernel<J, true, 2, kSchedInterleave, 8>(const KernelParams);
 UFC_INST_FIXED(1) UFC_INST_FIXED(2) UFC_INST_FIXED(3) UFC_INST_FIXED(4) UFC_INST_FIXED(5) UFC_INST_FIXED(6)
 
 
-const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves) {
-  if (abl == 0 && depth == 2 && sched == kSchedInterleave && waves == 8) {  // the product kernel
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int sched, int waves) {
+  if (depth == 2 && sched == kSchedInterleave && waves == 8) {  // the product kernel
     switch (J) {
 #define UFC_PICK_FIXED(JJ)                                                                          \
   case JJ:                                                                                          \
-    return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 2, 0, kSchedInterleave, 8>          \
-                : (const void*)frame_crc_fixed_kernel<JJ, false, 2, 0, kSchedInterleave, 8>;
+    return seal ? (const void*)frame_crc_fixed_kernel<JJ, true, 2, kSchedInterleave, 8>          \
+                : (const void*)frame_crc_fixed_kernel<JJ, false, 2, kSchedInterleave, 8>;
       UFC_PICK_FIXED(1) UFC_PICK_FIXED(2) UFC_PICK_FIXED(3) UFC_PICK_FIXED(4) UFC_PICK_FIXED(5) UFC_PICK_FIXED(6)
 #undef UFC_PICK_FIXED
       default: return nullptr;

@@ -361,9 +361,6 @@ __device__ __forceinline__ void load_set(const uint8_t* sbase, uint32_t voff, It
   }
 }
 
-constexpr int kLeanAblLoads = 1;
-constexpr int kLeanAblCompute = 2;
-
 // Stores written as inline asm: hipcc's wait-count model never sees them, so it keeps counting
 // loads only (a store it could see would make every later load wait vmcnt(0), since loads and
 // stores share vmcnt and may complete out of order).  A hidden store can only make a counted

@@ -7,9 +7,6 @@ namespace ufc_dev {
 constexpr int kModeVarlen = 1;  // frames from a CSR offsets array
 constexpr int kModeSeal = 2;    // write the BE32 trailer instead of validating it
 constexpr int kModeFreeze = 4;  // fixed-length frames whose block count is not a multiple of JC
-// (mode bits 8 and 16 were ablation variants of measurement builds; no kernel instantiates them)
-constexpr int kModeAblateCompute = 8;
-constexpr int kModeAblateLoads = 16;
 
 constexpr int kBlockThreads = 1024;          // one workgroup per CU, 16 waves
 constexpr int kLdsBytes = 131072 + 32768;    // chain tables + nibble tables
@@ -36,7 +33,7 @@ bool config_available(int jc);
 // Lean fixed-length kernel (frame_len >= 4, J = ceil((frame_len + 4) / 256) in 1..6); one
 // workgroup per CU owning a contiguous range of 4-frame sets, spread over its waves by `sched`;
 // `depth` sets in flight per wave.  Only the product configuration is instantiated (interleaved,
-// 8 waves, depth 2, abl 0); other arguments return nullptr.
+// 8 waves, depth 2); other arguments return nullptr.
 constexpr int kLeanDepthDefault = 2;
 // Results stay in registers until a wave's range is done: at most 16 * kLeanRuns sets per wave,
 // i.e. a launch covers at most (waves in the grid) * 16 * kLeanRuns * 4 frames (host-chunked).
@@ -50,7 +47,7 @@ constexpr int kSchedRange = 0;
 constexpr int kSchedClaim = 1;
 constexpr int kSchedInterleave = 2;
 constexpr int kLeanSchedDefault = kSchedInterleave;
-const void* fixed_kernel_symbol(int J, bool seal, int depth, int abl, int sched, int waves);
+const void* fixed_kernel_symbol(int J, bool seal, int depth, int sched, int waves);
 constexpr int kRunFrames = 64;
 // Variable-length kernel with 8 lanes per frame (frame_crc_varlen8.hip): CSR offsets (p.offsets,
 // n + 1) or (start, end) pairs (p.offsets holds 2n words, p.frame_len the buffer length); each run of

@@ -63,34 +63,24 @@ struct DevBytes {
   }
 };
 
-// The walk's reader: the frame's first HEAD bytes come from one load issued with the frame's other
-// first reads (HEAD = 16: kind, the data header's fields and the first datagram's size bytes, every
-// field of an ack frame's header; HEAD = 8: bytes 0..7), the rest as DevBytes.  The product walk uses
-// HEAD = 8: round 4's 16-byte head failed at random (one data frame per ~200k, a different one each
-// run) and its cause is not shown (profiles/EXPERIMENTS.md), so it stays out (it bought
-// ~2 %: 0.419 against 0.4105 ms).  head_byte keeps every shift amount in range.
-typedef unsigned int u32x4_h __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(1), aligned(1))) u32x4_h g_u32x4_h;
-template <uint32_t HEAD = 16>
+// The walk's reader: the frame's first 8 bytes come from one load issued with the frame's other
+// first reads (kind and the data header's fields), the rest as DevBytes.  (Round 4's 16-byte head,
+// which also held the first datagram's size bytes, failed at random -- one data frame per ~200k, a
+// different one each run -- and is gone: ADVICE r4, profiles/EXPERIMENTS.md "walk head" for the
+// ISA comparison.)  head_byte keeps every shift amount in range.
 struct DevBytesHead {
-  static_assert(HEAD == 16 || HEAD == 8, "head bytes");
   const uint8_t* p;
-  uint64_t w0, w1;  // bytes 0..7 and 8..15, little-endian
-  uint32_t held;    // bytes 0 .. held-1 in w0/w1: 16, 8 or 0
+  uint64_t w0;    // bytes 0..7, little-endian
+  uint32_t held;  // bytes 0 .. held-1 in w0: 8 or 0
   __device__ static DevBytesHead load(const uint8_t* q, uint32_t len) {  // (any byte address: unaligned access mode)
-    DevBytesHead r{q, 0ull, 0ull, 0u};
-    if (HEAD == 16 && len >= 16) {
-      const u32x4_h v = *(g_u32x4_h*)q;
-      r.w0 = (uint64_t)v.x | ((uint64_t)v.y << 32);
-      r.w1 = (uint64_t)v.z | ((uint64_t)v.w << 32);
-      r.held = 16;
-    } else if (len >= 8) {
+    DevBytesHead r{q, 0ull, 0u};
+    if (len >= 8) {
       r.w0 = *(g_u64_a1*)q;
       r.held = 8;
     }
     return r;
   }
-  __device__ uint32_t held_byte(uint32_t i) const { return head_byte(w0, w1, i); }
+  __device__ uint32_t held_byte(uint32_t i) const { return head_byte(w0, 0ull, i); }
   __device__ uint32_t operator()(uint32_t i) const {
     if (i < held) return held_byte(i);
     return *(const __attribute__((address_space(1))) uint8_t*)(p + i);
@@ -204,7 +194,7 @@ __global__ __launch_bounds__(kParseThreads) void parse_walk_pool_kernel(const ui
     uint64_t a;
     const uint32_t len = frame_len32(offsets, i, a);
     ufc_frame_info info;
-    const DevBytesHead<8> rd = DevBytesHead<8>::load(bytes + a, len);
+    const DevBytesHead rd = DevBytesHead::load(bytes + a, len);
     const bool ok = ufc_codec::read_frame_to(rd, len, valid[i] != 0, info,
                                              PoolSink{slots + t, pool, &pool_ctr, &head, &tail, &full}, kPosSlots);
     const uint32_t cnt = ok ? info.item_count : 0u;

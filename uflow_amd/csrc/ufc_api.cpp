@@ -29,6 +29,7 @@ struct ufc_ctx {
   uint32_t* d_nib32 = nullptr;
   uint32_t G = 0;
   int last_hip_error = 0;
+  std::atomic<int> stalled_comms{0};  // communicators of this context that stalled (ufc_internal::note_stall)
   // host-buffer path (ufc_validate_host_varlen): device staging, reused across calls
   uint8_t* d_stage = nullptr;
   size_t d_stage_cap = 0;
@@ -150,9 +151,9 @@ int lean_fixed_blocks(const ufc_ctx* ctx, uint64_t frame_len, uint64_t stride, u
 // front_ok: the bytes before the batch's first frame are readable (a later part of a larger batch).
 int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp, hipStream_t stream,
                       bool front_ok = false) {
-  const int depth = ufc_dev::kLeanDepthDefault, abl = 0, waves = ufc_dev::kLeanWavesDefault;
+  const int depth = ufc_dev::kLeanDepthDefault, waves = ufc_dev::kLeanWavesDefault;
   const int sched = ufc_dev::kLeanSchedDefault;
-  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, abl, sched, waves);
+  const void* fn = ufc_dev::fixed_kernel_symbol(J, seal, depth, sched, waves);
   if (!fn) return UFC_ERR_INVALID_ARG;
   kp.chain_tab = ctx->d_chain;
   kp.nib_img = ctx->d_nib;
@@ -401,6 +402,13 @@ int ufc_ctx_release_stream(ufc_ctx* ctx, void* stream) {
 
 int ufc_ctx_destroy(ufc_ctx* ctx) {
   if (!ctx) return UFC_OK;
+  if (ctx->stalled_comms.load() > 0) {
+    // A stalled communicator's all-reduce is still pending on the device (ufc_comm_set_timeout): every
+    // hipFree / hipStreamDestroy below would synchronize with it and never return.  The device memory
+    // and streams are left to process exit; the handle is gone.
+    delete ctx;
+    return UFC_ERR_COMM;
+  }
   {
     DeviceGuard g(ctx->device >= 0 ? ctx->device : 0);
     if (ctx->d_chain) (void)hipFree(ctx->d_chain);
@@ -443,6 +451,10 @@ int ufc_internal::ctx_device(const ufc_ctx* ctx) { return ctx ? ctx->device : -1
 
 void ufc_internal::note_hip_error(ufc_ctx* ctx, int e) {
   if (ctx) ctx->last_hip_error = e;
+}
+
+void ufc_internal::note_stall(ufc_ctx* ctx) {
+  if (ctx) ctx->stalled_comms.fetch_add(1);
 }
 
 int ufc_internal::crc_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame_len, size_t n,

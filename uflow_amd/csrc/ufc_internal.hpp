@@ -18,5 +18,9 @@ int crc_fixed(ufc_ctx* ctx, const uint8_t* d_frames, size_t stride, size_t frame
               uint8_t* d_valid_out, hipStream_t stream, bool front_ok);
 int ctx_device(const ufc_ctx* ctx);
 void note_hip_error(ufc_ctx* ctx, int e);
+// A communicator on this context stalled (a peer missed the status agreement's deadline): an RCCL
+// all-reduce stays pending on the device for good, so ufc_ctx_destroy must not free device memory
+// (hipFree synchronizes the device and would wait for it).
+void note_stall(ufc_ctx* ctx);
 
 }  // namespace ufc_internal

@@ -193,8 +193,17 @@ int abort_comm(ufc_comm* comm, int rc) {
 // asynchronous error, up to the communicator's deadline (ufc_comm_set_timeout).  A peer that has not
 // joined by then fails the call with UFC_ERR_COMM and leaves the communicator stalled: nothing is
 // aborted (ncclCommAbort measured not to return while the peer's side of the all-reduce is missing),
-// the pending all-reduce and its buffers stay as they are, every later call returns UFC_ERR_COMM, and
-// the caller ends the process (teardown at process exit).
+// the pending all-reduce and its buffers stay as they are, every later call returns UFC_ERR_COMM, the
+// context records the stall (ufc_ctx_destroy then leaves the device memory to process exit), and the
+// caller ends the process.
+//
+// Two rounds: the status all-reduce, then a one-word commit all-reduce.  A rank whose
+// deadline passes in round 1 never enqueues round 2.  A peer that joins later completes round 1 against
+// the stalled rank's pending all-reduce -- and would otherwise go on to queue its gather against a rank
+// that is gone -- but its round 2 then finds no partner: it stalls at its own deadline and fails with
+// UFC_ERR_COMM too.  So a late peer fails like the early one instead of hanging in its gather.  (Once
+// every rank has finished round 1 they are all present; round 2 only misses its deadline on a rank if a
+// peer dies in between.)
 // UFC_SHARD_TRACE=1: progress of the status agreement on stderr (diagnosing a peer that never joins).
 bool shard_trace() {
   static const bool on = [] {
@@ -213,12 +222,19 @@ bool shard_trace() {
     }                                                         \
   } while (0)
 
-int agree_status(ufc_comm* comm, int local_rc) {
-  if (comm->nranks == 1) return local_rc;
+// Mark the communicator stalled (and its context: ufc_ctx_destroy must not wait for the device).
+int stall(ufc_comm* comm) {
+  comm->stalled = true;
+  comm->broken = true;
+  ufc_internal::note_stall(comm->ctx);
+  return UFC_ERR_COMM;
+}
+
+// One round: word `in` of this rank -> max over the ranks into comm->h_status[1], waiting up to the
+// deadline.  UFC_OK, or an error (the communicator aborted or stalled).
+int ctl_round(ufc_comm* comm, int32_t in, int round) {
   const Rccl& r = rccl();
-  DeviceGuard g(ufc_internal::ctx_device(comm->ctx));  // (the control stream's device, whatever the caller's)
-  UFC_TRACE("agree_status: local %d, enqueueing", local_rc);
-  comm->h_status[0] = local_rc != UFC_OK ? 1 : 0;
+  comm->h_status[0] = in;
   comm->h_status[1] = -1;
   hipError_t e = hipMemcpyAsync(comm->d_status, comm->h_status, 4, hipMemcpyHostToDevice, comm->ctl_stream);
   if (e != hipSuccess) {
@@ -228,7 +244,7 @@ int agree_status(ufc_comm* comm, int local_rc) {
   const ncclResult_t nr = r.AllReduce(comm->d_status, comm->d_status, 1, ncclInt32, ncclMax, comm->ctl,
                                       comm->ctl_stream);
   if (nr != ncclSuccess) return abort_comm(comm, nccl_fail(comm, nr));
-  UFC_TRACE("agree_status: all-reduce enqueued");
+  UFC_TRACE("agree_status: round %d all-reduce enqueued", round);
   if ((e = hipMemcpyAsync(comm->h_status + 1, comm->d_status, 4, hipMemcpyDeviceToHost, comm->ctl_stream)) !=
       hipSuccess) {
     ufc_internal::note_hip_error(comm->ctx, (int)e);
@@ -247,16 +263,26 @@ int agree_status(ufc_comm* comm, int local_rc) {
       return abort_comm(comm, nccl_fail(comm, ae));
     if (comm->timeout_ms > 0 && (spin & 63) == 0 &&
         std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(comm->timeout_ms)) {
-      UFC_TRACE("agree_status: no answer from every peer in %d ms: stalled", comm->timeout_ms);
-      comm->stalled = true;
-      comm->broken = true;
-      return UFC_ERR_COMM;
+      if (hipStreamQuery(comm->ctl_stream) == hipSuccess) break;  // (done meanwhile)
+      UFC_TRACE("agree_status: round %d, no answer from every peer in %d ms: stalled", round, comm->timeout_ms);
+      return stall(comm);
     }
     if (spin > 1000) std::this_thread::sleep_for(std::chrono::microseconds(spin > 20000 ? 1000 : 20));
   }
-  UFC_TRACE("agree_status: agreed %d", comm->h_status[1]);
+  return UFC_OK;
+}
+
+int agree_status(ufc_comm* comm, int local_rc) {
+  if (comm->nranks == 1) return local_rc;
+  DeviceGuard g(ufc_internal::ctx_device(comm->ctx));  // (the control stream's device, whatever the caller's)
+  UFC_TRACE("agree_status: local %d, enqueueing", local_rc);
+  if (const int rc = ctl_round(comm, local_rc != UFC_OK ? 1 : 0, 1)) return rc;
+  const int32_t agreed = comm->h_status[1];
+  UFC_TRACE("agree_status: agreed %d", agreed);
+  if (const int rc = ctl_round(comm, 0, 2)) return rc;  // commit: every rank got through round 1
+  UFC_TRACE("agree_status: committed");
   if (local_rc != UFC_OK) return local_rc;
-  return comm->h_status[1] != 0 ? UFC_ERR_PEER : UFC_OK;
+  return agreed != 0 ? UFC_ERR_PEER : UFC_OK;
 }
 
 // The gate of one chunk's frames, results into the rank's outputs at `dst`.
