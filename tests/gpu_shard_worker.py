@@ -107,10 +107,16 @@ def late_peer():
     frames = synth.fixed_frames(hi - lo, L, synth.SEED_CONFIG4, device=dev)
     crc = torch.full((total if rank == 0 else hi - lo,), -1, dtype=torch.int32, device=dev)
     gate.set_timeout(3000)
+
+    def say(what):  # progress on stderr (the test prints each rank's stderr tail on a hang)
+        print(f"[late_peer rank {rank} {time.monotonic():.2f}] {what}", file=sys.stderr, flush=True)
+
+    say("comm ready")
     if rank == 1:  # late: only after rank 0 has given up
         t0 = time.monotonic()
         while not os.path.exists(flag0) and time.monotonic() - t0 < 90:
             time.sleep(0.05)
+    say("calling crc_sharded")
     t0 = time.monotonic()
     try:
         gate.crc_sharded(frames, L, total, crc, None, root=0)
@@ -118,10 +124,13 @@ def late_peer():
     except NativeError as e:
         code = e.code
     t_call = round(time.monotonic() - t0, 3)
+    say(f"crc_sharded returned {code} after {t_call} s")
     t0 = time.monotonic()
     gate.close()
+    say("communicator closed")
     eng.close()  # must return although an all-reduce is pending on the device
     t_close = round(time.monotonic() - t0, 3)
+    say(f"context closed ({t_close} s)")
     mine = {"rank": rank, "code": code, "t_call": t_call, "t_close": t_close}
     if rank == 0:
         with open(flag0, "w") as f:

@@ -337,3 +337,49 @@ def test_parse_large_batch(engine):
     bad = np.nonzero((got.view(np.uint8).reshape(n, -1) != ref.view(np.uint8).reshape(n, -1)).any(1))[0]
     assert bad.size == 0, f"{bad.size} frame infos differ from the host parse, first frames {bad[:8]}"
     assert k == ref_items.size
+
+
+def test_varlen_long_frames_deferred(engine):
+    """Frames of 0..8192 B (the reference's test generators and crc_flips go up to 8192 B,
+    serial/mod.rs:932-992, 1054-1080) and a few of 64 KiB - 1 MiB: the ones longer than the
+    variable-length kernel's 13-line fast path are deferred by its byte path to the second launch
+    (frame_crc_long8_kernel).  Every length near the 13/14-line edge at every start offset mod 128, a
+    seal, CSR and reversed (start, end) pairs, each against the oracle, called back to back (the
+    per-stream counts the second launch zeroes)."""
+    rng = np.random.default_rng(0x5EED8192)
+    edge = np.arange(1520, 1680)  # the 13/14-line edge (P = ceil((len + r + 4) / 128), r = (start - 4) mod 128)
+    lens = np.concatenate([rng.integers(0, 8193, size=200_000), np.tile(edge, 130),
+                           rng.integers(0, 64, size=20_000), np.array([65_536, 200_001, 1 << 20, 1533, 1532])])
+    rng.shuffle(lens)
+    lens = lens.astype(np.uint64)
+    n = lens.size
+    off = np.zeros(n + 1, np.uint64)
+    off[1:] = np.cumsum(lens)
+    host = rng.integers(0, 256, size=int(off[-1]) + 3, dtype=np.uint8)
+    ref_sealed = host.copy()
+    oracle.seal_varlen_mt(ref_sealed[: int(off[-1])], off, THREADS)
+    d = torch.from_numpy(host).to(DEV)
+    offs = torch.from_numpy(off.view(np.int64)).to(DEV)
+    crc_s = torch.full((n,), -1, dtype=torch.int32, device=DEV)
+    engine.seal_varlen(d, offs, crc_out=crc_s)
+    torch.cuda.synchronize()
+    assert torch.equal(d, torch.from_numpy(ref_sealed).to(DEV)), "seal differs from the oracle's"
+    live = np.nonzero(lens >= 5)[0]
+    flipped = live[::7]
+    ref_sealed[off[flipped] + (lens[flipped] - 1) // 2] ^= 0x04
+    d = torch.from_numpy(ref_sealed).to(DEV)
+    ref_crc, ref_valid = oracle.validate_varlen_mt(ref_sealed[: int(off[-1])], off, THREADS)
+    for rep in range(3):
+        crc, valid = engine.crc_varlen(d, offs)
+        torch.cuda.synchronize()
+        _compare(crc, valid, ref_crc, ref_valid, f"long frames, CSR, call {rep}")
+    assert int(ref_valid.sum()) == live.size - flipped.size
+    rev = np.arange(n - 1, -1, -1)
+    pairs = np.stack([off[:-1][rev], off[1:][rev]], axis=1).astype(np.int64)
+    crc, valid = engine.crc_pairs(d, torch.from_numpy(pairs).to(DEV))
+    torch.cuda.synchronize()
+    _compare(crc, valid, ref_crc[rev], ref_valid[rev], "long frames, pairs")
+    got = _host(crc_s).view(np.uint32)  # the seal's CRC words: the CRC of each frame's first len - 4 bytes
+    sealed_ok = lens >= 4
+    ref_c, _ = oracle.validate_varlen_mt(host[: int(off[-1])], off, THREADS)
+    assert np.array_equal(got[sealed_ok], ref_c[sealed_ok])

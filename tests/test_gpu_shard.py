@@ -89,7 +89,7 @@ def test_sharded_varlen_world1_config3(engine, gate):
     assert int(ref_valid.sum()) == n - len(range(0, n, 1001))
 
 
-def _run_worker(world, args, timeout):
+def _run_worker(world, args, timeout, extra_env=None):
     """`world` ranks of tests/gpu_shard_worker.py started directly (env:// rendezvous on 127.0.0.1),
     each in a process group of its own with its output in a file: on a timeout every rank's group is
     killed and the output read so far names the step that hung."""
@@ -100,6 +100,7 @@ def _run_worker(world, args, timeout):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     base = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LOCAL_WORLD_SIZE=str(world))
+    base.update(extra_env or {})
     cmd = [sys.executable, os.path.join(repo, "tests", "gpu_shard_worker.py")] + args
     procs, files = [], []
     for r in range(world):
@@ -185,7 +186,7 @@ def test_sharded_late_peer():
     deadline (the commit round finds no partner) instead of queueing a gather that hangs.  Both ranks
     then close the communicator and the context: ufc_ctx_destroy returns at once although an
     all-reduce stays pending on the device (tests/gpu_shard_worker.py --late-peer)."""
-    p = _run_worker(2, ["--late-peer"], 150)
+    p = _run_worker(2, ["--late-peer"], 150, extra_env={"UFC_SHARD_TRACE": "1"})
     objs = re.findall(r"\{\"late_peer\".*\}", p.stdout)
     assert len(objs) == 1, (p.stdout[-2000:], p.stderr[-2000:])
     j = json.loads(objs[0])

@@ -71,7 +71,7 @@ def main():
     if varlen:
         n = int(os.environ.get("VL_N", 10_000_000))
         rng = np.random.default_rng(0x5EED0002)
-        lens = rng.integers(64, 1501, n).astype(np.uint64)
+        lens = rng.integers(int(os.environ.get("VL_MIN", 64)), int(os.environ.get("VL_MAX", 1500)) + 1, n).astype(np.uint64)
         o = np.zeros(n + 1, np.uint64)
         o[1:] = np.cumsum(lens)
         offs = torch.from_numpy(o.view(np.int64)).to(dev)

@@ -3,7 +3,9 @@ scratch tree, `file:old=>new` substitutions applied (each must match), compiled 
 flags.  A/B measurement only (tools/ab_inproc.py); the product library is never touched.
 `file@path` replaces a source file of the copy with another file (e.g. an earlier round's, from git show);
 VARIANT_FLAGS (environment) adds hipcc flags; VARIANT_NO_MLLVM drops the named `-mllvm` options.
-Usage: python tools/build_variant.py <name> 'frame_crc_varlen8.hip:old=>new' 'frame_parse.hip@/tmp/old.hip' ..."""
+`--ref <git ref>` first takes uflow_amd/csrc and include/ from that commit instead of the working tree (the
+previous round's library, for an A/B against it).
+Usage: python tools/build_variant.py <name> [--ref <commit>] 'frame_crc_varlen8.hip:old=>new' 'frame_parse.hip@/tmp/old.hip' ..."""
 import os
 import shutil
 import subprocess
@@ -19,8 +21,14 @@ from uflow_amd import _build  # noqa: E402
 def main():
     name, subs = sys.argv[1], sys.argv[2:]
     d = tempfile.mkdtemp(prefix="ufc_var_")
-    shutil.copytree(os.path.join(REPO, "uflow_amd", "csrc"), os.path.join(d, "uflow_amd", "csrc"))
-    shutil.copytree(os.path.join(REPO, "include"), os.path.join(d, "include"))
+    if subs[:1] == ["--ref"]:
+        ref, subs = subs[1], subs[2:]
+        arch = subprocess.run(["git", "-C", REPO, "archive", ref, "uflow_amd/csrc", "include"], check=True,
+                              capture_output=True).stdout
+        subprocess.run(["tar", "-x", "-C", d], input=arch, check=True)
+    else:
+        shutil.copytree(os.path.join(REPO, "uflow_amd", "csrc"), os.path.join(d, "uflow_amd", "csrc"))
+        shutil.copytree(os.path.join(REPO, "include"), os.path.join(d, "include"))
     for sub in subs:
         if "@" in sub and ":" not in sub.split("@", 1)[0]:
             fn, src = sub.split("@", 1)

@@ -25,6 +25,11 @@ struct KernelParams {
   uint32_t G;                 // A^-4(~0)
   uint32_t* ctr;              // lean fixed kernel: per-workgroup claim counters (zero at launch)
   uint32_t front_ok;          // lean fixed kernel: the pad bytes before frame 0 are readable
+  // Variable-length kernel: frames longer than its 13-line fast path (and in range) are left to a
+  // second launch (frame_crc_long8_kernel): their indices go to defer_list (workgroup b's from entry
+  // 64 * its first run on), workgroup b's count to defer_counts[b].  Null: they take the byte path.
+  uint32_t* defer_list;
+  uint32_t* defer_counts;
 };
 
 // Kernel entry for (JC 256-byte blocks per pipelined part, mode); nullptr if not instantiated.
@@ -55,6 +60,10 @@ constexpr int kRunFrames = 64;
 // 32-slot nibble image.  varlen8_waves(): the workgroup's waves (one workgroup per CU).
 const void* varlen8_kernel_symbol(bool seal, bool pairs);
 int varlen8_waves();
+// The second launch over the frames the variable-length kernel deferred (p.defer_list / p.defer_counts of
+// a first launch with the same p and `blocks` workgroups): one workgroup per first-launch workgroup,
+// reading only its count when that is zero.
+const void* long8_kernel_symbol(bool seal, bool pairs);
 // Slot layout -> (start, end) pairs on the device: pairs[2i] = i * stride, pairs[2i+1] = i * stride
 // + lens[i] (ufc_validate_host_slots_async).
 int slots_to_pairs(const uint32_t* d_lens, uint64_t stride, uint64_t n, uint64_t* d_pairs, void* stream);

@@ -52,6 +52,18 @@ constexpr uint32_t kNoSet = 0xFFFFFFFFu;   // a wave's set sequence past its las
 // The workgroup's run counter: nibble-image row 127, column 63 (rows 80..127 of columns 32..63 are
 // never read).
 constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
+// Deferred frames: the workgroup's list counter and p.defer_list / p.defer_counts (read where they are
+// used, from LDS: no scalar registers held across the loop).  Staged by thread 1023, which sets them.
+constexpr uint32_t kV8DefAddr = (127u * 64u + 62u) * 4u;
+constexpr uint32_t kV8ListPtrAddr = (127u * 64u + 58u) * 4u, kV8CountsPtrAddr = (127u * 64u + 56u) * 4u;
+constexpr uint32_t kV8CrcPtrAddr = (127u * 64u + 54u) * 4u, kV8ValidPtrAddr = (127u * 64u + 52u) * 4u;
+// A pointer kept in LDS at byte `addr` (the kernel's static LDS starts at address 0), read at the point of
+// use: a volatile ds_read_b64 (lgkmcnt only), never hoisted into registers held across the loop.
+template <typename T>
+__device__ __forceinline__ T* lds_ptr(uint32_t addr) {
+  typedef T* volatile __attribute__((address_space(3))) * LdsPtrSlot;
+  return *(LdsPtrSlot)(uintptr_t)addr;
+}
 
 // Per-lane geometry of a frame on the fast path (one VGPR): r = (frame start - 4) mod 128 [0,7) (the
 // window starts at the 128-byte line holding G's first byte, r bytes before it), len [7,18), index
@@ -119,6 +131,19 @@ __device__ __forceinline__ uint32_t group_lin8_rot(const Lane8& L, const Chains&
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
   v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
   return v;
+}
+
+// A^-t of every group's lin, one nibble per lane: lane col of a group looks up A^-t of lin's nibble
+// col in its own column 32 + (lane & 31) of the 32-slot image (rows 16 (t + 1) + nibble value; a
+// half-wave's 32 lanes read 32 banks) and the group sums its 8 terms over DPP.
+__device__ __forceinline__ uint32_t unshift8(const Lane8& L, uint32_t lin, uint32_t t) {
+  if (__builtin_amdgcn_ballot_w64(t != 0) == 0) return lin;
+  const uint32_t nib = (lin >> (4u * L.col)) & 15u;
+  uint32_t r = *(const uint32_t*)(L.lds + ((t << 12) | (nib << 8)) + (L.K & 0xFFu) + (4096u + 128u));
+  r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  return t ? r : lin;
 }
 
 // Front-fix table in LDS: for p = 0..20 bytes of a 16-byte piece before its frame, the mask M of
@@ -478,22 +503,16 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   auto store_run = [&](uint32_t run) {  // hidden stores (see frame_crc_dev.hpp)
     const uint64_t f = (uint64_t)run * kRunFrames + (acc_qv & 63u);
     if (!(acc_qv & 0x40000000u) && f < nfr) {
-      if (p.crc_out) st_u32_hidden(p.crc_out + f, acc_crc);
-      if (!SEAL && p.valid_out) st_u8_hidden(p.valid_out + f, acc_qv >> 31);
+      // (the output pointers from LDS, read here: no scalar registers held across the loop for them)
+      uint32_t* const co = lds_ptr<uint32_t>(kV8CrcPtrAddr);
+      if (co) st_u32_hidden(co + f, acc_crc);
+      if (!SEAL) {
+        uint8_t* const vo = lds_ptr<uint8_t>(kV8ValidPtrAddr);
+        if (vo) st_u8_hidden(vo + f, acc_qv >> 31);
+      }
     }
   };
-  // A^-t of every group's lin, one nibble per lane: lane col of a group looks up A^-t of lin's nibble
-  // col in its own column 32 + (lane & 31) of the 32-slot image (rows 16 (t + 1) + nibble value; a
-  // half-wave's 32 lanes read 32 banks) and the group sums its 8 terms over DPP.
-  auto unshift = [&](uint32_t lin, uint32_t t) -> uint32_t {
-    if (__builtin_amdgcn_ballot_w64(t != 0) == 0) return lin;
-    const uint32_t nib = (lin >> (4u * L.col)) & 15u;
-    uint32_t r = *(const uint32_t*)(L.lds + ((t << 12) | (nib << 8)) + (L.K & 0xFFu) + (4096u + 128u));
-    r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    return t ? r : lin;
-  };
+  auto unshift = [&](uint32_t lin, uint32_t t) -> uint32_t { return unshift8(L, lin, t); };
 
   // Fast set.  The stream of a frame is its window with the bytes before G zeroed, G, the data, the
   // trailer as zeros, up to the end of the word holding the frame's last byte (e: that word's slot,
@@ -531,18 +550,18 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     // hold as component a & 3: each lane picks the group's component and ds_bpermute gathers them.
     const int u = (int)zo - 128 * (int)(P - 1u);
     const uint32_t a1 = min((uint32_t)(u + 4) >> 2, 31u), a0 = max((uint32_t)(u + 4) >> 2, 1u) - 1u;
-    uint32_t tw_p = 0u, tw0 = 0u, tw1 = 0u;  // word 31 of line P - 2, words a0 and a1 of line P - 1
+    uint32_t tw_p = 0u, tw0 = 0u, tw1 = 0u;  // word 31 of line P - 2 (in the group's lane 0), the trailer's words
     auto pick = [](const uint4& x, uint32_t k) {
       const uint32_t lo = (k & 1u) ? x.y : x.x, hi = (k & 1u) ? x.w : x.z;
       return (k & 2u) ? hi : lo;
     };
     auto trailer_words = [&](int s, const uint4& x) {
       if constexpr (!SEAL) {
-        const uint32_t gb = L.lane & ~7u;
-        if (s == 11) {
-          tw_p = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + 7u) * 4u), (int)x.w);
-        } else if (s == 12) {
-          tw0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + (a0 >> 2)) * 4u), (int)pick(x, a0 & 3u));
+        if (s == 11) {  // line P - 2's last word, into the group's lane 0 (row_half_mirror: no lane index)
+          tw_p = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x.w, 0x141, 0xF, 0xF, false);
+        } else if (s == 12) {  // the trailer's first word: from line P - 2 (lane 0) when it starts there
+          const uint32_t gb = L.lane & ~7u;
+          tw0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + (a0 >> 2)) * 4u), (int)(u < 0 ? tw_p : pick(x, a0 & 3u)));
           tw1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + (a1 >> 2)) * 4u), (int)pick(x, a1 & 3u));
         }
       }
@@ -599,7 +618,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     }
     const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
     const uint32_t crc = ~unshift(group_lin8_rot(L, c, e), t);
-    const uint32_t tr = __builtin_amdgcn_alignbyte(tw1, u < 0 ? tw_p : tw0, (uint32_t)u & 3u);
+    const uint32_t tr = __builtin_amdgcn_alignbyte(tw1, tw0, (uint32_t)u & 3u);
     const uint32_t ok = (!SEAL && w_len(geo) >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
     if (SEAL && L.col == 0u) {  // BE32 trailer: one (unaligned) dword store per frame
       // (non-temporal trailer stores measured slower: 1.912 against 1.874 ms)
@@ -621,7 +640,29 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
       r = take_raw(T, q);
     }
     const uint64_t a = (uint64_t)r.x | ((uint64_t)r.y << 32);
-    const bool dead = (r.w >> 31) != 0;
+    // Longer than the fast path, window inside the buffer: to the workgroup's list for the second launch
+    // (frame_crc_long8_kernel), which stores its results; here it counts as dead.
+    const uint32_t rr = ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - 4u) & 127u;
+    const bool defer = (r.w >> 31) == 0 && r.z >= 4u && r.z < 0x40000000u && r.z + rr > 128u * 13u - 4u &&
+                       a >= 4u + rr;
+    // (a deferred frame's 8 lanes all store its index into its slot: no per-column lane mask)
+    const uint64_t dm = __builtin_amdgcn_ballot_w64(defer);
+    if (dm != 0) {
+      uint32_t base = 0;
+      if (L.lane == 0)
+        base = __hip_atomic_fetch_add((uint32_t*)(lds + kV8DefAddr), (uint32_t)__builtin_popcountll(dm) >> 3,
+                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+      const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(dm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)dm, 0u)) >> 3;
+      uint32_t* const dl = lds_ptr<uint32_t>(kV8ListPtrAddr);  // (this workgroup's part of the list)
+      if (defer) *as_global<g_u32w>(dl + base + rk) = (q >> 3) * kRunFrames + (r.w & 63u);
+      if (L.lane == 0) {
+        uint32_t* const dc = lds_ptr<uint32_t>(kV8CountsPtrAddr);  // (this workgroup's count)
+        __hip_atomic_fetch_add(as_global<g_u32w>(dc), (uint32_t)__builtin_popcountll(dm) >> 3, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    const bool dead = (r.w >> 31) != 0 || defer;
     const uint32_t len = dead ? 0u : r.z;
     const FrameDesc d = make_desc(a, len);
     uint32_t nb = 0;
@@ -690,7 +731,14 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   fixtab_store(lds, p.G);  // (then an LDS-only barrier, as in stage_store: the prefetches stay in flight)
   // Runs WR0 .. WR0 + WAVES - 1 are taken statically.  (Set by the thread whose stage_store wrote
   // the word, after it: program order, then the barrier below.)
-  if (threadIdx.x == 1023u % (WAVES * 64u)) *ctr = WAVES;
+  if (threadIdx.x == 1023u % (WAVES * 64u)) {
+    *ctr = WAVES;
+    *(uint32_t*)(lds + kV8DefAddr) = 0u;
+    *(uint32_t**)(lds + kV8ListPtrAddr) = p.defer_list + (uint64_t)WR0 * kRunFrames;
+    *(uint32_t**)(lds + kV8CountsPtrAddr) = p.defer_counts + blockIdx.x;
+    *(uint32_t**)(lds + kV8CrcPtrAddr) = p.crc_out;
+    *(uint8_t**)(lds + kV8ValidPtrAddr) = p.valid_out;
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -722,6 +770,166 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     SB = SBN;
     M = MN;
   }
+
+}
+
+// ---- Frames longer than the fast path (over 13 lines, 1532 B): the second launch ----
+// frame_crc_varlen8_kernel's byte path leaves them to this kernel (p.defer_list, p.defer_counts) instead
+// of running them byte-wise, since its loop's 128 VGPRs have no room for a line loop (a line-loop path
+// inside it cost config 3 0.3-0.45 %, profiles/EXPERIMENTS.md).  Workgroup b takes the frames workgroup b
+// of the first launch deferred (a workgroup with none reads its count and leaves before staging any
+// table) and zeroes its count for the next first launch.
+// Its waves claim chunks of 64 frames, order each chunk by line count (radix split passes, as the first
+// launch orders its runs), and run the chunk as sets of 8 frames, 8 lanes per frame: the same slot-chain
+// CRC over whole 128-byte lines of the same window (the line holding G's first byte to the line holding
+// the frame's last byte), right-aligned so that every frame's last line comes at the set's last step:
+// steps before a frame's line 0 load its line 0 again and are zeroed (its chains stay zero), line 0 is
+// front-fixed, the last two steps are masked at the end of the CRC'd data, and the trailer comes from the
+// last two lines' registers.  Four lines per frame are in flight (loads issued four steps ahead).
+constexpr int kL8Waves = 16;
+template <bool SEAL, bool PAIRS>
+__global__ __launch_bounds__(kL8Waves * 64) void frame_crc_long8_kernel(const KernelParams p, uint32_t main_blocks) {
+  constexpr int WAVES = kL8Waves;
+  const uint32_t cnt = __builtin_amdgcn_readfirstlane((int)p.defer_counts[blockIdx.x]);
+  if (cnt == 0) return;
+  __shared__ __attribute__((aligned(16))) char lds[kLdsBytes];
+  const StageSet<WAVES * 64> sr = stage_load<WAVES * 64>(p);
+  Lane8 L;
+  init_lane8(L, lds, p.G);
+  const uint64_t nfr = p.nframes;
+  const uint32_t nruns = (uint32_t)((nfr + kRunFrames - 1) / kRunFrames);
+  const uint64_t region = (uint64_t)((uint64_t)nruns * blockIdx.x / main_blocks) * kRunFrames;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* const ctr = (uint32_t*)(lds + kV8CtrAddr);
+  stage_store<WAVES * 64>(sr, lds);
+  fixtab_store(lds, p.G);
+  if (threadIdx.x == 1023u % (WAVES * 64u)) *ctr = WAVES;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  // Every wave has read the count (before the barrier): zero it for the next first launch on this
+  // stream, whose byte path adds to it (a vector store).
+  if (threadIdx.x == 0) st_u32_hidden(p.defer_counts + blockIdx.x, 0u);
+  const uint32_t nchunks = (cnt + 63u) / 64u;
+  const uint64_t* offs = p.offsets;
+  for (uint32_t c = wid; c < nchunks;) {
+    // ---- the chunk's frames, one per lane, ordered by line count ----
+    const uint32_t here = min(cnt - 64u * c, 64u);
+    const bool live = L.lane < here;
+    const uint32_t f = live ? p.defer_list[region + 64u * c + L.lane] : 0u;
+    const uint64_t a = *as_global<g_u64>(offs + (PAIRS ? 2 * (uint64_t)f : f));
+    const uint64_t b = *as_global<g_u64>(offs + (PAIRS ? 2 * (uint64_t)f + 1 : f + 1));
+    const uint32_t len = (uint32_t)(b - a);  // (>= 1533 and < 2^30: the first launch's rule)
+    const uint32_t r0 = ((uint32_t)(uintptr_t)p.bytes + (uint32_t)a - 4u) & 127u;
+    const uint32_t P0 = (len + r0 + 131u) >> 7;
+    uint32_t v = ((live ? min(P0, 127u) : 255u) << 6) | L.lane;
+#pragma unroll
+    for (uint32_t bit = 6; bit < 14; bit++) {  // stable LSD radix split by key (8 bits)
+      const bool one = ((v >> bit) & 1u) != 0;
+      const uint64_t m = __builtin_amdgcn_ballot_w64(one);
+      const uint32_t ob = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      const uint32_t pos = one ? 64u - (uint32_t)__builtin_popcountll(m) + ob : L.lane - ob;
+      v = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos * 4u), (int)v);
+    }
+    const int src = (int)((v & 63u) * 4u);  // sorted position L.lane holds frame (lane) src / 4
+    const uint32_t s_f = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)f);
+    const uint32_t s_alo = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)a);
+    const uint32_t s_ahi = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)(uint32_t)(a >> 32));
+    const uint32_t s_len = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)len);
+    // next chunk (claimed now, used after this one)
+    uint32_t nxt = 0;
+    if (L.lane == 0) nxt = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    nxt = (uint32_t)__builtin_amdgcn_readfirstlane((int)nxt);
+
+    const uint32_t nsets = (here + 7u) / 8u;
+    for (uint32_t q = 0; q < nsets; q++) {
+      // group g: sorted position 8 q + g (positions past the chunk repeat its last frame, unstored)
+      const uint32_t sp = min(8u * q + L.grp, here - 1u);
+      const bool dead = 8u * q + L.grp >= here;
+      const int sl = (int)(sp * 4u);
+      const uint32_t fr = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)s_f);
+      const uint64_t fa = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)s_alo) |
+                          ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)s_ahi) << 32);
+      const uint32_t fl = (uint32_t)__builtin_amdgcn_ds_bpermute(sl, (int)s_len);
+      const uint32_t r = ((uint32_t)(uintptr_t)p.bytes + (uint32_t)fa - 4u) & 127u;
+      const uint32_t front = r + 4u, zo = fl + r, P = (zo + 131u) >> 7;
+      uint32_t Pmax = 0, Pmin = 0xFFFFFFFFu;
+#pragma unroll
+      for (int g = 0; g < 8; g++) {
+        const uint32_t x = (uint32_t)__builtin_amdgcn_readlane((int)P, 8 * g);
+        Pmax = max(Pmax, x);
+        Pmin = min(Pmin, x);
+      }
+      const uint32_t P4 = (Pmax + 3u) & ~3u;  // steps: a multiple of 4, every frame's last line at step P4 - 1
+      const uint32_t sh = P4 - P;             // frame line j = step - sh
+      const uint8_t* const wbase = p.bytes + (fa - 4u - r) + 16u * L.col;
+      auto load_line = [&](uint32_t k) -> uint4 {  // step k's line, clamped into the frame's window
+        const int j = (int)k - (int)sh;
+        const uint32_t jc = (uint32_t)min(max(j, 0), (int)P - 1);
+        const u32x4 x = __builtin_nontemporal_load(as_global<g_u32x4>(wbase + 128u * jc));
+        return make_uint4(x.x, x.y, x.z, x.w);
+      };
+      const int lim0 = (int)zo - (int)(16u * L.col);
+      const int uu = (int)zo - 128 * (int)(P - 1u);  // the trailer's first byte in line P - 1 (-3 .. 124)
+      const uint32_t a1 = min((uint32_t)(uu + 4) >> 2, 31u), a0 = max((uint32_t)(uu + 4) >> 2, 1u) - 1u;
+      auto pick = [](const uint4& x, uint32_t k) {
+        const uint32_t lo = (k & 1u) ? x.y : x.x, hi = (k & 1u) ? x.w : x.z;
+        return (k & 2u) ? hi : lo;
+      };
+      uint32_t tw_p = 0u, tw0 = 0u, tw1 = 0u;
+      Chains ch{0u, 0u, 0u, 0u, 0u};
+      uint4 X[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) X[u] = load_line((uint32_t)u);
+      const uint32_t pre_end = P4 - Pmin + 2u;  // steps up to a frame's line 1 (zeros, front fix, G's tail)
+      for (uint32_t k0 = 0; k0 < P4; k0 += 4u) {
+        const bool last = k0 + 4u == P4;  // (uniform)
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint32_t k = k0 + (uint32_t)u;
+          uint4 x = X[u];
+          if (!last) X[u] = load_line(k + 4u);
+          if (k < pre_end) {
+            const int j = (int)k - (int)sh;
+            const bool z = j < 0;  // (component selects: a select of whole vectors goes through the stack)
+            x = make_uint4(z ? 0u : x.x, z ? 0u : x.y, z ? 0u : x.z, z ? 0u : x.w);
+            if (__builtin_amdgcn_ballot_w64(j == 0) != 0) {
+              const uint4 fx = fix_piece(L.lds, x, (int)front - (int)(16u * L.col));
+              const bool l0 = j == 0;
+              x = make_uint4(l0 ? fx.x : x.x, l0 ? fx.y : x.y, l0 ? fx.z : x.z, l0 ? fx.w : x.w);
+            }
+            if (__builtin_amdgcn_ballot_w64(j == 1) != 0)
+              x.x = j == 1 ? fix_word(x.x, 128 + (int)(16u * L.col) - (int)front, L.G) : x.x;
+          }
+          if (last && u == 2) {  // line P - 2
+            if constexpr (!SEAL) tw_p = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(((L.lane & ~7u) + 7u) * 4u), (int)x.w);
+            chain4_masked(L, ch, x, lim0 - 128 * (int)(P - 2u));
+          } else if (last && u == 3) {  // line P - 1
+            if constexpr (!SEAL) {
+              const uint32_t gb = L.lane & ~7u;
+              tw0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + (a0 >> 2)) * 4u), (int)pick(x, a0 & 3u));
+              tw1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((gb + (a1 >> 2)) * 4u), (int)pick(x, a1 & 3u));
+            }
+            chain4_masked(L, ch, x, lim0 - 128 * (int)(P - 1u));
+          } else {
+            chain4(L, ch, x);
+          }
+        }
+      }
+      const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
+      const uint32_t crc = ~unshift8(L, group_lin8_rot(L, ch, e), t);
+      if (L.col == 0u && !dead) {
+        if (p.crc_out) st_u32_hidden(p.crc_out + fr, crc);
+        if constexpr (SEAL) {
+          st_u32_hidden((uint32_t*)(p.wbytes + fa + fl - 4u), __builtin_bswap32(crc));
+        } else {
+          const uint32_t tr = __builtin_amdgcn_alignbyte(tw1, uu < 0 ? tw_p : tw0, (uint32_t)uu & 3u);
+          if (p.valid_out) st_u8_hidden(p.valid_out + fr, __builtin_bswap32(tr) == crc ? 1u : 0u);
+        }
+      }
+    }
+    c = nxt;
+  }
 }
 
 // Product (round 5): 16 waves, one pipelined buffer each, one straight copy of the positions per entry
@@ -738,6 +946,18 @@ const void* varlen8_kernel_symbol(bool seal, bool pairs) {
   return seal ? (const void*)frame_crc_varlen8_kernel<true, false> : (const void*)frame_crc_varlen8_kernel<false, false>;
 }
 int varlen8_waves() { return kV8Waves; }
+
+template __global__ void frame_crc_long8_kernel<false, false>(const KernelParams, uint32_t);
+template __global__ void frame_crc_long8_kernel<true, false>(const KernelParams, uint32_t);
+template __global__ void frame_crc_long8_kernel<false, true>(const KernelParams, uint32_t);
+template __global__ void frame_crc_long8_kernel<true, true>(const KernelParams, uint32_t);
+
+const void* long8_kernel_symbol(bool seal, bool pairs) {
+  if (pairs)
+    return seal ? (const void*)frame_crc_long8_kernel<true, true> : (const void*)frame_crc_long8_kernel<false, true>;
+  return seal ? (const void*)frame_crc_long8_kernel<true, false> : (const void*)frame_crc_long8_kernel<false, false>;
+}
+
 
 __global__ __launch_bounds__(256) void slots_to_pairs_kernel(const uint32_t* lens, uint64_t stride, uint64_t n,
                                                               uint64_t* pairs) {

@@ -64,11 +64,13 @@ constexpr uint32_t kCtrSlots = 64;
 
 namespace {
 
-enum ScratchKind { kScratchParse = 0, kScratchAsyncSlots = 2, kScratchSealCrc = 3 };
+enum ScratchKind { kScratchParse = 0, kScratchAsyncSlots = 2, kScratchSealCrc = 3, kScratchDeferList = 4, kScratchDeferCounts = 5 };
 
 // The (kind, stream) scratch buffer of at least `need` bytes.  Growing waits for the work already
-// queued on that stream (the only user of the old buffer) before freeing it.
-hipError_t stream_scratch(ufc_ctx* ctx, int kind, hipStream_t stream, size_t need, void** out) {
+// queued on that stream (the only user of the old buffer) before freeing it.  *fresh (if given): the
+// buffer was (re)allocated by this call.
+hipError_t stream_scratch(ufc_ctx* ctx, int kind, hipStream_t stream, size_t need, void** out, bool* fresh = nullptr) {
+  if (fresh) *fresh = false;
   std::lock_guard<std::mutex> lk(ctx->scratch_mu);
   ufc_ctx::Scratch* sc = nullptr;
   for (auto& x : ctx->scratch)
@@ -87,6 +89,7 @@ hipError_t stream_scratch(ufc_ctx* ctx, int kind, hipStream_t stream, size_t nee
     }
     if ((e = hipMalloc(&sc->p, need)) != hipSuccess) return e;
     sc->cap = need;
+    if (fresh) *fresh = true;
   }
   *out = sc->p;
   return hipSuccess;
@@ -194,30 +197,51 @@ int launch_lean_fixed(ufc_ctx* ctx, int J, bool seal, ufc_dev::KernelParams& kp,
 // The sorted-runs kernel with 8 lanes per frame (frame_crc_varlen8.hip): one launch per chunk of
 // < 2^29 frames, each run of 64 frames sorted by piece count inside the kernel.  Any buffer size:
 // each set's loads are relative to its run's own base (a set whose frames lie 2 GB or more apart,
-// possible with pairs, runs on the kernel's byte path).
+// possible with pairs, runs on the kernel's byte path).  Frames longer than its 13-line fast path are
+// deferred by its byte path to a second launch on the same stream (frame_crc_long8_kernel): a per-stream
+// list of frame indices (4 B per frame of a chunk) and per-workgroup counts (zeroed once when allocated;
+// the second launch zeroes the counts it consumed).  A workgroup of the second launch with nothing
+// deferred reads its count and returns.
 int launch_varlen8(ufc_ctx* ctx, bool seal, bool pairs, ufc_dev::KernelParams& kp, hipStream_t stream) {
   const void* fn = ufc_dev::varlen8_kernel_symbol(seal, pairs);
-  if (!fn) return UFC_ERR_INVALID_ARG;
+  const void* fn_long = ufc_dev::long8_kernel_symbol(seal, pairs);
+  if (!fn || !fn_long) return UFC_ERR_INVALID_ARG;
   const int waves = ufc_dev::varlen8_waves();
   kp.chain_tab = ctx->d_chain128;
   kp.nib_img = ctx->d_nib32;
   kp.G = ctx->G;
   const uint64_t chunk = (uint64_t)1 << 29;  // (32-bit set indices: 8 per run of 64 frames)
   const uint64_t total = kp.nframes;
+  void* list = nullptr;
+  void* counts = nullptr;
+  bool fresh = false;
+  hipError_t e;
+  const uint64_t nmax = std::min(chunk, total);
+  if ((e = stream_scratch(ctx, kScratchDeferList, stream, (size_t)(nmax + 64) * 4, &list)) != hipSuccess ||
+      (e = stream_scratch(ctx, kScratchDeferCounts, stream, (size_t)ctx->ncu * 4, &counts, &fresh)) != hipSuccess)
+    return hip_fail(ctx, e);
+  if (fresh && (e = hipMemsetAsync(counts, 0, (size_t)ctx->ncu * 4, stream)) != hipSuccess) return hip_fail(ctx, e);
   for (uint64_t f0 = 0; f0 < total; f0 += chunk) {
     ufc_dev::KernelParams c = kp;
     c.nframes = std::min(chunk, total - f0);
     c.offsets = kp.offsets + (pairs ? 2 * f0 : f0);
     if (kp.crc_out) c.crc_out = kp.crc_out + f0;
     if (kp.valid_out) c.valid_out = kp.valid_out + f0;
+    c.defer_list = (uint32_t*)list;
+    c.defer_counts = (uint32_t*)counts;
     // one workgroup per CU, at least one run of 64 frames per wave
     const uint64_t nruns = (c.nframes + 63) / 64;
     uint64_t blocks = (nruns + waves - 1) / waves;
     if (blocks > (uint64_t)ctx->ncu) blocks = (uint64_t)ctx->ncu;
     if (blocks < 1) blocks = 1;
     void* args[] = {&c};
-    const hipError_t e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream);
-    if (e != hipSuccess) return hip_fail(ctx, e);
+    if ((e = hipLaunchKernel(fn, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args, 0, stream)) != hipSuccess)
+      return hip_fail(ctx, e);
+    uint32_t nb = (uint32_t)blocks;
+    void* args_long[] = {&c, &nb};
+    if ((e = hipLaunchKernel(fn_long, dim3((unsigned)blocks), dim3((unsigned)(waves * 64)), args_long, 0, stream)) !=
+        hipSuccess)
+      return hip_fail(ctx, e);
   }
   return UFC_OK;
 }
