@@ -239,8 +239,8 @@ def test_seal_varlen_shared_blocks(engine, shift):
     """Seals of frames packed tight: short neighbours (trailers a few bytes apart, many in one 64-byte
     block), trailers across a block edge, a batch at any address, and the bytes around the batch left
     alone.  Every trailer must equal the oracle's and no other byte may change, whatever store shape the
-    seal uses (round 5 measured whole-64-byte-block trailer writes and kept one dword store per frame,
-    DESIGN.md section 5.3)."""
+    seal uses (one dword store per frame in the product; whole-64-byte-block forms were measured and
+    not kept)."""
     rng = np.random.default_rng(60 + shift)
     lens = np.concatenate([rng.integers(4, 140, size=40_000), rng.integers(4, 1533, size=20_000),
                            rng.integers(60, 70, size=5_000)])

@@ -64,7 +64,14 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sp = ctypes.c_void_p(stream.cuda_stream)
     loaded = {path: load(path) for _, path, _ in variants}
-    libs = {name: (loaded[path], make_ctx(loaded[path], env)) for name, path, env in variants}
+    libs = {name: (loaded[path], make_ctx(loaded[path], {k: v for k, v in env.items() if not k.startswith("OPT")}))
+            for name, path, env in variants}
+    for name, path, env in variants:  # OPT<k>=<v>: ufc_ctx_set_option(ctx, k, v)
+        lib, ctx = libs[name]
+        for k, v in env.items():
+            if k.startswith("OPT"):
+                lib.ufc_ctx_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+                assert lib.ufc_ctx_set_option(ctx, int(k[3:]), int(v)) == 0, (name, k, v)
     g = torch.Generator(device=dev)
     g.manual_seed(0x5EED0001)
     crc = valid = offs = None
