@@ -40,6 +40,12 @@
 
 namespace ufc_dev {
 
+// Structured buffer load (index, offset): llvm.amdgcn.struct.ptr.buffer.load, which clang exposes no
+// builtin for.  Address = base + index * stride + voffset; an index at or past num_records (a
+// "negative" one included) loads zeros and makes no memory request.
+extern "C" __device__ u32x4 ufc_struct_buffer_load_b128(__amdgpu_buffer_rsrc_t rsrc, int vindex, int voffset,
+                                                        int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+
 namespace {
 
 constexpr int kV8Pieces = 13;              // fast path: windows of up to 13 lines (frames of 4..1532 B)
@@ -441,7 +447,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // Geometry of set q from its words: per-lane geometry, the lane's line-0 offset, the set facts, the
   // run base (the buffer offset of the loads' resource, minus a bias: the run's first frame's start,
   // or the buffer itself for flat pairs).
-  auto geometry = [&](uint32_t q, const Rec& r, uint32_t& voff0, Set8Meta& m, uint64_t& sb) -> uint32_t {
+  auto geometry = [&](uint32_t q, const Rec& r, uint32_t& voff0, Set8Meta& m, uint64_t& sb, uint32_t& p14) -> uint32_t {
     sb = r.sb;
     const uint32_t gu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.geo);
     const uint32_t hu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.wrel);
@@ -454,6 +460,10 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     // (the window start's low 7 bits: bytes + sb + start is 128-byte aligned)
     const uint32_t low7 = (0u - (uint32_t)(uintptr_t)p.bytes - (uint32_t)sb) & 127u;
     voff0 = live ? (((r.wrel & 0xFFFFFFu) << 7) | low7) + 16u * L.col : kV8Oob;
+    // the record index of slot 0 (+ k for slot k): P - 14, or -14 for a set with no loads (every record
+    // "negative"); opaque, so that the select stays here once per set and is not pushed into the slots
+    p14 = (live ? w_P(r.geo) : 0u) - 14u;
+    asm("" : "+v"(p14));
     return r.geo;
   };
   // The set's loads (struct Buf13): line 0 (slot 0) and the last line (slot 12), the lines the frame
@@ -467,7 +477,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // while the position's last XORs still read the slot, the load goes into other registers, and each
   // straight copy of the positions ends with a different register assignment, moved back at the
   // loop's merge behind a vmcnt(1) wait)
-  auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, Buf13& b, const Chains* dep) {
+  auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, uint32_t p14, Buf13& b, const Chains* dep) {
     const uint32_t P = w_P(geo), front = w_r(geo) + 4u;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
     if (k == 0) {
@@ -476,21 +486,18 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
       b.x[0] = make_uint4(v.x, v.y, v.z, v.w);
       return;
     }
-    // slot k at base + 128 k (an out-of-range voff0 keeps base out of range wherever it is used:
-    // k + P >= 14; the run base's bias keeps base itself above 0)
-    const uint32_t base = voff0 + 128u * P - 128u * 13u;
-    uint32_t vo = (uint32_t)k + P >= 14u ? base : kV8Oob;
-    // (opaque to the optimizer: otherwise it pushes the slot's constant 128 k through the select, one
-    // more add and one more register per slot, instead of the load's immediate offset)
+    // slot k = line k - 13 + P, as record k - 14 + P of 128-byte records from the window's line 1 (a
+    // structured load: one add per slot; a line before line 1 is a "negative" record, out of range:
+    // zeros, no request; p14 from geometry()).
+    const __amdgpu_buffer_rsrc_t rss =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 128, (int)0x7FFFFFF0, 0x00020000);
+    uint32_t idx = p14 + (uint32_t)k;
     if (dep)
-      asm("" : "+v"(vo) : "v"(dep->v0), "v"(dep->v1), "v"(dep->v2), "v"(dep->v3));
+      asm("" : "+v"(idx) : "v"(dep->v0), "v"(dep->v1), "v"(dep->v2), "v"(dep->v3));
     else
-      asm("" : "+v"(vo));
-    u32x4 v;
-    if (k == kV8Pieces - 1)
-      v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxShared);
-    else
-      v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + 128u * (uint32_t)k), 0, kV8AuxInterior);
+      asm("" : "+v"(idx));
+    const u32x4 v = ufc_struct_buffer_load_b128(rss, (int)idx, (int)(voff0 + 128u), 0,
+                                                k == kV8Pieces - 1 ? kV8AuxShared : kV8AuxInterior);
     b.x[k] = make_uint4(v.x, v.y, v.z, v.w);
   };
 
@@ -721,9 +728,10 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   {  // prologue: the first set's geometry and loads, the second set's record
     QG = next_q();
     const Rec r0 = load_rec(QG);
-    GE = geometry(QG, r0, VO, M, SB);
+    uint32_t P14;
+    GE = geometry(QG, r0, VO, M, SB, P14);
 #pragma unroll
-    for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, B, nullptr);
+    for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, P14, B, nullptr);
     QO = next_q();
     O = load_rec(QO);
   }
@@ -747,15 +755,15 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // (a wave's sets are valid up to its first kNoSet)
   while (QG != kNoSet) {
     // the next set: geometry from its record; the record after it
-    uint32_t VN;
+    uint32_t VN, PN;
     uint64_t SBN;
     Set8Meta MN;
     const uint32_t QN = QO;
-    const uint32_t GN = geometry(QN, O, VN, MN, SBN);
+    const uint32_t GN = geometry(QN, O, VN, MN, SBN, PN);
     QO = next_q();
     O = load_rec(QO);
     __builtin_amdgcn_sched_barrier(0);
-    auto issue = [&](int k, const Chains* dep = nullptr) { load_slot(k, VN, GN, SBN, B, dep); };
+    auto issue = [&](int k, const Chains* dep = nullptr) { load_slot(k, VN, GN, SBN, PN, B, dep); };
     if (!M.slow) {
       compute(QG, GE, M, B, VO, SB, issue);
     } else {
