@@ -80,8 +80,7 @@ __device__ __forceinline__ T* lds_ptr(uint32_t addr) {
 // facts: kV8PenultData (no frame's trailer starts in its line P - 2: that line holds CRC'd data only
 // wherever it is a frame's) and kV8G1 (a frame's G reaches into line 1: r >= 125).
 __device__ __forceinline__ uint32_t w_r(uint32_t g) { return g & 127u; }
-__device__ __forceinline__ uint32_t w_len(uint32_t g) { return (g >> 7) & 2047u; }
-__device__ __forceinline__ uint32_t w_zo(uint32_t g) { return w_len(g) + w_r(g); }
+__device__ __forceinline__ uint32_t w_zo(uint32_t g) { return (g >> 7) & 2047u; }
 __device__ __forceinline__ uint32_t w_P(uint32_t g) { return (w_zo(g) + 131u) >> 7; }
 __device__ __forceinline__ uint32_t w_orig(uint32_t g) { return (g >> 18) & 63u; }
 constexpr uint32_t kV8PenultData = 1u << 25, kV8G1 = 1u << 26;
@@ -334,8 +333,8 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     const uint64_t rel64 = a - sb;
     FGeo g;
     g.wrel = (uint32_t)rel64 - 4u - r;  // window start (128-byte aligned in memory)
-    g.bad = !live || len < 4u || P > (uint32_t)kV8Pieces || a < 4u + r || rel64 >= (uint64_t)kV8Limit || rel64 < 512u;
-    g.geo = r | (min(len, 2047u) << 7) | (L.lane << 18);
+    g.bad = !live || len < 5u || P > (uint32_t)kV8Pieces || a < 4u + r || rel64 >= (uint64_t)kV8Limit || rel64 < 512u;
+    g.geo = r | (min(zo, 2047u) << 7) | (L.lane << 18);
     return g;
   };
   auto run_base = [&](uint64_t a) -> uint64_t {
@@ -478,7 +477,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // straight copy of the positions ends with a different register assignment, moved back at the
   // loop's merge behind a vmcnt(1) wait)
   auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, uint32_t p14, Buf13& b, const Chains* dep) {
-    const uint32_t P = w_P(geo), front = w_r(geo) + 4u;
+    const uint32_t front = w_r(geo) + 4u;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
     if (k == 0) {
       const uint32_t vo = (16u * L.col + 16u <= front) ? kV8Oob : voff0;
@@ -503,9 +502,10 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
 
   // ---- results of the current run: lane (g, col = t) <- set t's frame g; qv = orig | valid << 31
   uint32_t acc_crc = 0, acc_qv = 0;
-  auto record = [&](uint32_t t, uint32_t crc, uint32_t qv) {
-    acc_crc = (L.col == t) ? crc : acc_crc;
-    acc_qv = (L.col == t) ? qv : acc_qv;
+  auto record = [&](uint32_t t, uint32_t crc, uint32_t qv) {  // (lanes col == t: a scalar mask, no compare)
+    const bool mine = __builtin_amdgcn_inverse_ballot_w64(0x0101010101010101ull << t);
+    acc_crc = mine ? crc : acc_crc;
+    acc_qv = mine ? qv : acc_qv;
   };
   auto store_run = [&](uint32_t run) {  // hidden stores (see frame_crc_dev.hpp)
     const uint64_t f = (uint64_t)run * kRunFrames + (acc_qv & 63u);
@@ -626,7 +626,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
     const uint32_t crc = ~unshift(group_lin8_rot(L, c, e), t);
     const uint32_t tr = __builtin_amdgcn_alignbyte(tw1, tw0, (uint32_t)u & 3u);
-    const uint32_t ok = (!SEAL && w_len(geo) >= 5u && __builtin_bswap32(tr) == crc) ? 1u : 0u;
+    const uint32_t ok = (!SEAL && __builtin_bswap32(tr) == crc) ? 1u : 0u;  // (fast-path frames have >= 5 B)
     if (SEAL && L.col == 0u) {  // BE32 trailer: one (unaligned) dword store per frame
       // (non-temporal trailer stores measured slower: 1.912 against 1.874 ms)
       uint32_t* const ta = (uint32_t*)((uint8_t*)p.wbytes + sb + (voff0 + zo));
