@@ -1,6 +1,6 @@
 """Secondary measurements for DESIGN.md (BASELINE.json configs 3, 4-per-GPU and 5, the seal and the
 parse), one JSON line each.  Not the driver's bench (bench.py is); run on the GPU box:
-    python tools/bench_configs.py [--only varlen,shard,seal,seal_varlen,parse,parse_mtu,host] [--reps 20]
+    python tools/bench_configs.py [--only varlen,shard,seal,seal_varlen,parse,parse_mtu,gate_tg,host] [--reps 20]
 
   varlen   config 3: 10M frames, lengths U[64,1500] (splitmix64, seed 0x5EED0002), CSR offsets,
            device-resident; every frame checked against the oracle; CPU baseline of the same loop
@@ -210,15 +210,8 @@ def seal_varlen(eng, dev, reps, n=10_000_000):
                  valid_after_seal=ok)
 
 
-def parse(eng, dev, reps, n=1_000_000, mtu=False):
-    """ufc_parse_batch_varlen over n real uflow frames (data frames with datagrams, acks, syncs):
-    600 distinct frames from the codec oracle, tiled.  The generators are the reference's test
-    generators (random_data_frame, serial/mod.rs:932-992), which ignore the frame size limit: 38 % of
-    these frames are longer than MAX_FRAME_SIZE (1472 B, src/lib.rs:291-294), up to 7.5 KB, and take
-    the gate's byte path.  mtu=True keeps only frames a uflow receiver can get (<= MAX_FRAME_SIZE: the
-    emitters' limit, half_connection/emit.rs:69, and the receive buffer, server/mod.rs:595): each data
-    frame keeps the longest prefix of its datagrams that fits, as the emitter packs a frame until the
-    next datagram would not fit (emit.rs:69)."""
+def parse_batch(n, mtu):
+    """The parse workloads' batch (host arrays): 600 distinct frames from the codec oracle, tiled (see parse)."""
     import random
     from oracle import codec as C
     rng = random.Random(5)
@@ -230,14 +223,61 @@ def parse(eng, dev, reps, n=1_000_000, mtu=False):
     base = [fit(C.random_data_frame(rng) if i % 3 == 0 else C.receive_side_data_frame(rng)
                 if i % 3 == 1 else C.random_ack_frame(rng, 20)) for i in range(600)]
     assert not mtu or max(len(f) for f in base) <= C.MAX_FRAME_SIZE
-    frames = [base[i % 600] for i in range(n)]
-    lens = np.array([len(f) for f in frames], dtype=np.int64)
+    lens = np.array([len(base[i % 600]) for i in range(n)], dtype=np.int64)
     offsets = np.zeros(n + 1, dtype=np.int64)
     offsets[1:] = np.cumsum(lens)
     blob = np.frombuffer(b"".join(base), dtype=np.uint8)
-    bo = np.zeros(601, dtype=np.int64)
-    bo[1:] = np.cumsum([len(f) for f in base])
     data = np.concatenate([blob] * (n // 600 + 1))[: int(offsets[-1])]
+    return data, offsets, lens
+
+
+def gate_tg(eng, dev, reps, n=1_000_000):
+    """The variable-length gate alone on the parse workload's test-generator batch (38 % of frames over
+    13 lines: the first launch's byte path defers them to frame_crc_long8_kernel), every frame against
+    the oracle; the generic kernel timed beside it."""
+    data, offsets, lens = parse_batch(n, False)
+    d = torch.from_numpy(data).to(dev)
+    o = torch.from_numpy(offsets).to(dev)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    valid = torch.empty(n, dtype=torch.uint8, device=dev)
+    fn = lambda: eng.crc_varlen(d, o, crc_out=crc, valid_out=valid)  # noqa: E731
+    fn()
+    torch.cuda.synchronize()
+    settle(fn)
+    med, mean = timed(fn, reps)
+    total = int(offsets[-1])
+    from uflow_amd import _native as N
+    saved = eng.get_option(N.UFC_OPT_VARLEN_KERNEL)
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, N.UFC_VARLEN_GENERIC)
+    crc2 = torch.empty(n, dtype=torch.int32, device=dev)
+    valid2 = torch.empty(n, dtype=torch.uint8, device=dev)
+    fn2 = lambda: eng.crc_varlen(d, o, crc_out=crc2, valid_out=valid2)  # noqa: E731
+    fn2()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(crc, crc2) and torch.equal(valid, valid2))
+    settle(fn2, 300)
+    med2, _ = timed(fn2, reps)
+    eng.set_option(N.UFC_OPT_VARLEN_KERNEL, saved)
+    extra = {}
+    if CHECK:
+        ref_crc, ref_valid = oracle.validate_varlen_mt(data, offsets.astype(np.uint64), min(64, threads()))
+        extra["bit_exact_all_frames"] = bool(np.array_equal(crc.cpu().numpy().view(np.uint32), ref_crc) and
+                                             np.array_equal(valid.cpu().numpy(), ref_valid))
+    return rates("gate on the parse test-generator batch (1M uflow frames, 38 % over 1532 B)", total,
+                 total + 8 * (n + 1) + 5 * n, med, mean, None, frames=n, over_13_lines=float(np.mean(lens > 1532)),
+                 other_kernel="generic", other_kernel_ms=round(med2, 4), other_equal_results=same, **extra)
+
+
+def parse(eng, dev, reps, n=1_000_000, mtu=False):
+    """ufc_parse_batch_varlen over n real uflow frames (data frames with datagrams, acks, syncs):
+    600 distinct frames from the codec oracle, tiled.  The generators are the reference's test
+    generators (random_data_frame, serial/mod.rs:932-992), which ignore the frame size limit: 38 % of
+    these frames are longer than MAX_FRAME_SIZE (1472 B, src/lib.rs:291-294), up to 7.5 KB, and take
+    the gate's byte path.  mtu=True keeps only frames a uflow receiver can get (<= MAX_FRAME_SIZE: the
+    emitters' limit, half_connection/emit.rs:69, and the receive buffer, server/mod.rs:595): each data
+    frame keeps the longest prefix of its datagrams that fits, as the emitter packs a frame until the
+    next datagram would not fit (emit.rs:69)."""
+    data, offsets, lens = parse_batch(n, mtu)
     d = torch.from_numpy(data).to(dev)
     o = torch.from_numpy(offsets).to(dev)
     _, valid = eng.crc_varlen(d, o)

@@ -26,7 +26,12 @@ SHARD = 12_500_000
 WORKLOADS = {
     "bench": [("config 2 validate (bench line)", "frame_crc_fixed_kernel<6, false", N2 * (L2 + 5)),
               ("read-only streaming ceiling probe over the same 1.5 GB", "read_stream_kernel", N2 * L2 // 1024 * 1024)],
-    "varlen": [("config 3 validate", "frame_crc_varlen8_kernel<false, false", "varlen")],
+    "varlen": [("config 3 validate", "frame_crc_varlen8_kernel<false, false", "varlen"),
+               ("config 3 validate, second launch (frames over 13 lines: none here, each workgroup reads its "
+                "count and returns)", "frame_crc_long8_kernel<false, false", None)],
+    "gate_tg": [("gate on the test-generator batch, first launch", "frame_crc_varlen8_kernel<false, false", None),
+                ("gate on the test-generator batch, second launch (the 38 % of frames over 13 lines)",
+                 "frame_crc_long8_kernel<false, false", None)],
     "shard": [("config 4 per-GPU shard validate (3 launches of 4.17M frames)", "frame_crc_fixed_kernel<6, false",
                SHARD // 3 * (L2 + 5))],
     "seal": [("config 2 seal, one kernel (product: each workgroup's trailers after its reads)",
@@ -34,7 +39,8 @@ WORKLOADS = {
              ("config 2 seal, two passes (comparison): pass 1 (CRC words)", "frame_crc_fixed_kernel<6, false",
               N2 * (L2 + 4)),
              ("config 2 seal, two passes (comparison): pass 2 (trailer stores)", "seal_scatter_kernel", N2 * 8)],
-    "seal_varlen": [("config 3 seal", "frame_crc_varlen8_kernel<true, false", "seal_varlen")],
+    "seal_varlen": [("config 3 seal", "frame_crc_varlen8_kernel<true, false", "seal_varlen"),
+                    ("config 3 seal, second launch (none over 13 lines)", "frame_crc_long8_kernel<true, false", None)],
     "parse": [("parse walk (test-generator workload)", "parse_walk", None),
               ("parse emit (test-generator workload)", "parse_emit", None)],
     "parse_mtu": [("parse walk (frames <= MAX_FRAME_SIZE)", "parse_walk", None),
@@ -112,7 +118,7 @@ def main():
         json.dump(summary, f, indent=1)
     b = summary.get("config 2 validate (bench line)")
     if b and b["fetch_bytes_per_dispatch"] and b["write_bytes_per_dispatch"]:
-        out = {"frames": N2, "frame_len": L2, "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 0, 2, 8, 4224>",
+        out = {"frames": N2, "frame_len": L2, "kernel": "ufc_dev::frame_crc_fixed_kernel<6, false, 2, 2, 8, 4224>",
                "fetch_bytes_per_launch": b["fetch_bytes_per_dispatch"],
                "write_bytes_per_launch": b["write_bytes_per_dispatch"],
                "hbm_bytes_per_launch": b["fetch_bytes_per_dispatch"] + b["write_bytes_per_dispatch"],
