@@ -367,6 +367,10 @@ def main():
         # socket transport (loopback), which runs the same ncclSend/ncclRecv calls of ufc_crc_sharded.
         local = 0
         os.environ["NCCL_HOSTID"] = f"ufc-one-device-rank{rank}"
+        # One hardware queue per rank: 8 processes x HIP's default 4 queues oversubscribe the GPU's queue
+        # slots, and the scheduler then time-slices even idle queues (round 6: n1_sharded_ref 3980 GiB/s with
+        # the default, 5919 with one queue per rank; the 8-rank step 108 against 61 ms).  (Before any HIP call.)
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", "1")
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         os.environ.setdefault("NCCL_IB_DISABLE", "1")
     torch.cuda.set_device(local)
