@@ -226,6 +226,100 @@ __global__ __launch_bounds__(768) void vset(const uint8_t* bytes, const uint64_t
   (void)live;
 }
 
+// Round 6: the product's load schedule without its compute.  One set buffer of 13 slots per wave (slot 0 =
+// line 0, slot k >= 1 = line k - 13 + P, the last line default policy, the lines between non-temporal),
+// software-pipelined as the product: slot k of the next set is issued as soon as the current set has
+// consumed slot k.  The sets (8 frames each, sorted by line count within runs of 64 on the host) come as
+// one 16-byte record per frame, read two sets ahead.  STEPS: each consumed slot also runs the product's
+// chain step (4 perm + 4 ds_read_b32 + 2 xor3 per word from LDS; the values are not a CRC).  Question: is
+// the one-buffer schedule itself, or the compute on it, what holds config 3's gate above the 2-buffer
+// probe's 1.18 ms?
+struct SetRec {
+  uint32_t ws, fr, P, wsh;  // window start (low, high 32 bits of the offset in the allocation)
+};
+template <int WAVES, bool STEPS>
+__global__ __launch_bounds__(WAVES * 64) void vpipe(const uint8_t* bytes, const SetRec* recs, uint32_t nsets,
+                                                    uint32_t* out) {
+  __shared__ char lds[160 * 1024];
+  constexpr int SL = 13;
+  const uint32_t lane = threadIdx.x & 63, c = lane & 7, g = lane >> 3;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t W = gridDim.x * WAVES, w = blockIdx.x * WAVES + wid;
+  const uint32_t S0 = (uint64_t)nsets * w / W, S1 = (uint64_t)nsets * (w + 1) / W;
+  // (the wave's base: its first window start - 512; window starts relative to it fit 32 bits)
+  // (read as a vector load and made uniform with readfirstlane: a scalar load of the two words was
+  // combined with a sign-extending s_bfe_i64 of the low word, a wrong base past 2 GB -- round 6's fault)
+  const u32x4 r0v = *(const u32x4*)(recs + (uint64_t)S0 * 8);
+  const uint64_t wbase = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r0v.x) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)r0v.w) << 32);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(bytes + wbase - 512), 0, 0x7FFFFFF0, 0x00020000);
+  for (uint32_t i = threadIdx.x; i < 160 * 1024 / 4; i += WAVES * 64) ((uint32_t*)lds)[i] = i * 0x9E3779B1u;
+  __syncthreads();
+  const uint32_t K = ((lane & 31u) * 4u) | (((lane & 31u) * 4u + 128u) << 8) | (1u << 24);
+  uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, acc = 0;
+  auto step = [&](uint32_t v, uint32_t x) -> uint32_t {
+    const char* t = lds + 32768;
+    const uint32_t r0 = *(const uint32_t*)(t + __builtin_amdgcn_perm(v, K, 0x0C020400u));
+    const uint32_t r1 = *(const uint32_t*)(t + __builtin_amdgcn_perm(v, K, 0x0C020501u));
+    const uint32_t r2 = *(const uint32_t*)(t + __builtin_amdgcn_perm(v, K, 0x0C030600u));
+    const uint32_t r3 = *(const uint32_t*)(t + __builtin_amdgcn_perm(v, K, 0x0C030701u));
+    return __builtin_amdgcn_bitop3_b32(__builtin_amdgcn_bitop3_b32(r0, r1, r2, 0x96), r3, x, 0x96);
+  };
+  auto rec = [&](uint32_t si) -> SetRec {  // (unconditional: the array holds 2 padding sets past the last)
+    const u32x4 v = *(const u32x4*)(recs + (uint64_t)si * 8 + g);
+    return SetRec{(uint32_t)(((uint64_t)v.w << 32 | v.x) - wbase + 512u), v.y, v.z, 0u};
+  };
+  // dep: the value the consuming step has just produced; the load is tied after it (as the product's
+  // load_slot), so the loads go out in slot order and the waits stay counted
+  auto load = [&](int s, const SetRec& r, uint32_t dep, bool live = true) -> u32x4 {
+    const uint32_t o0 = live && r.P > 0 ? r.ws + 16 * c : kOob;
+    uint32_t vo;
+    if (s == 0) {
+      vo = 16 * c + 16 <= r.fr ? kOob : o0;
+    } else {
+      const int line = s - 13 + (int)r.P;
+      vo = line >= 1 ? o0 + 128u * (uint32_t)line : kOob;
+    }
+    asm("" : "+v"(vo) : "v"(dep));
+    if (s == 0 || s == 12) return __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, 0);
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, 2);
+  };
+  u32x4 A[SL];
+  {
+    const SetRec r0 = rec(S0);
+#pragma unroll
+    for (int s = 0; s < SL; s++) A[s] = load(s, r0, 0u);
+  }
+  // records of sets si + 1 and si + 2 in two registers used in turn (no copy of a pending load's result)
+  SetRec ra = rec(S0 + 1), rb = rec(S0 + 2);
+  auto body = [&](const SetRec& rn, bool live) {
+#pragma unroll
+    for (int s = 0; s < SL; s++) {
+      const u32x4 x = A[s];
+      if (STEPS) {
+        c0 = step(c0, x.x);
+        c1 = step(c1, x.y);
+        c2 = step(c2, x.z);
+        c3 = step(c3, x.w);
+      } else {
+        acc ^= x.x ^ x.y ^ x.z ^ x.w;
+      }
+      A[s] = load(s, rn, STEPS ? (c0 ^ c3) : acc, live);
+      asm volatile("" ::: "memory");  // (one slot at a time, as the product's position blocks)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  for (uint32_t si = S0; si < S1; si += 2) {
+    body(ra, si + 1 < S1);
+    ra = rec(si + 3);
+    if (si + 1 >= S1) break;
+    body(rb, si + 2 < S1);
+    rb = rec(si + 4);
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc ^ c0 ^ c1 ^ c2 ^ c3;
+}
+
 __global__ __launch_bounds__(512) void stream(const uint8_t* bytes, uint64_t nbytes, uint32_t* out) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -249,6 +343,9 @@ __global__ __launch_bounds__(512) void stream(const uint8_t* bytes, uint64_t nby
 }
 
 uint64_t g_total = 0;
+SetRec* g_recs = nullptr;
+uint32_t g_nsets = 0;
+uint8_t* g_alloc = nullptr;
 
 int main() {
   const uint32_t n = 10000000;
@@ -269,6 +366,29 @@ int main() {
   bytes = alloc + 4096;
   (void)hipMemcpy(doff, off.data(), 8 * (n + 1), hipMemcpyHostToDevice);
   g_total = total;
+  {  // vpipe's set records: runs of 64 frames sorted by line count (stable), 8 frames per set
+    const uint32_t nsets = (n + 7) / 8;
+    std::vector<SetRec> recs((size_t)(nsets + 4) * 8, SetRec{0, 0, 0, 0});  // (+ padding sets, P = 0)
+    const uint64_t ab = (uint64_t)(bytes - alloc);
+    for (uint32_t r0 = 0; r0 < n; r0 += 64) {
+      std::vector<std::pair<uint32_t, uint32_t>> kf;
+      for (uint32_t i = r0; i < std::min(n, r0 + 64); i++) {
+        const uint64_t a = off[i] + ab, b = off[i + 1] + ab;  // (offsets within the allocation)
+        const uint64_t ws = (a - 4) & ~127ull;
+        kf.push_back({(uint32_t)((b - ws + 127) / 128), i});
+      }
+      std::stable_sort(kf.begin(), kf.end(), [](auto& x, auto& y) { return x.first < y.first; });
+      for (size_t j = 0; j < kf.size(); j++) {
+        const uint32_t i = kf[j].second;
+        const uint64_t a = off[i] + ab, ws = (a - 4) & ~127ull;
+        recs[(size_t)(r0 / 8 + j / 8) * 8 + j % 8] = SetRec{(uint32_t)ws, (uint32_t)(a - ws), kf[j].first, (uint32_t)(ws >> 32)};
+      }
+    }
+    if (hipMalloc(&g_recs, recs.size() * sizeof(SetRec)) != hipSuccess) return 1;
+    (void)hipMemcpy(g_recs, recs.data(), recs.size() * sizeof(SetRec), hipMemcpyHostToDevice);
+    g_nsets = nsets;
+    g_alloc = alloc;
+  }
   printf("policy probe: %u frames, %.3f GB\n", n, total / 1e9);
   struct V {
     const char* name;
@@ -294,7 +414,11 @@ int main() {
             PP(12, 0, false), PP(12, 1, true),
 #define PS(S_) {"set slots=" #S_, [](const uint8_t* b, const uint64_t* o, uint32_t nn, uint32_t* ou) { \
      hipLaunchKernelGGL((vset<S_>), dim3(256), dim3(768), 0, 0, b, o, nn, ou); }}
-            PS(3), PS(0), PS(1), PS(2)};
+            PS(1),
+#define PQ(W_, S_) {"pipe waves=" #W_ " steps=" #S_, [](const uint8_t* b, const uint64_t* o, uint32_t nn, uint32_t* ou) { \
+     (void)b; (void)o; (void)nn; \
+     hipLaunchKernelGGL((vpipe<W_, S_>), dim3(256), dim3(W_ * 64), 0, 0, g_alloc, g_recs, g_nsets, ou); }}
+            PQ(16, false), PQ(16, true), PQ(12, false), PQ(12, true)};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);

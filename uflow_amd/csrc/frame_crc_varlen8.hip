@@ -55,6 +55,9 @@ constexpr uint32_t kV8Limit = 0x7FF00000u;  // fast-path window offsets stay bel
 constexpr int kV8AuxShared = 0;            // a frame's first and last line: default policy (shared)
 constexpr int kV8AuxInterior = 2;          // the lines in between: non-temporal (read once)
 constexpr uint32_t kNoSet = 0xFFFFFFFFu;   // a wave's set sequence past its last claimed run
+// Slot loads k >= 1 (load_slot): record counts 3 + k against the index 16 - P; 29 lines off the base.
+constexpr int kV8SlotRecords = 3;
+constexpr uint64_t kV8SlotBase = 29u * 128u;
 // The workgroup's run counter: nibble-image row 127, column 63 (rows 80..127 of columns 32..63 are
 // never read).
 constexpr uint32_t kV8CtrAddr = (127u * 64u + 63u) * 4u;
@@ -143,8 +146,8 @@ __device__ __forceinline__ uint32_t group_lin8_rot(const Lane8& L, const Chains&
 // half-wave's 32 lanes read 32 banks) and the group sums its 8 terms over DPP.
 __device__ __forceinline__ uint32_t unshift8(const Lane8& L, uint32_t lin, uint32_t t) {
   if (__builtin_amdgcn_ballot_w64(t != 0) == 0) return lin;
-  const uint32_t nib = (lin >> (4u * L.col)) & 15u;
-  uint32_t r = *(const uint32_t*)(L.lds + ((t << 12) | (nib << 8)) + (L.K & 0xFFu) + (4096u + 128u));
+  const uint32_t nib = __builtin_amdgcn_ubfe(lin, 4u * L.col, 4u);
+  uint32_t r = *(const uint32_t*)(L.lds + ((nib << 8) | ((t << 12) | (L.K & 0xFFu))) + (4096u + 128u));
   r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
   r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
   r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);  // row_half_mirror
@@ -159,16 +162,28 @@ __device__ __forceinline__ uint32_t unshift8(const Lane8& L, uint32_t lin, uint3
 constexpr int kFixEntries = 21;
 __device__ __forceinline__ uint32_t fixtab_addr(uint32_t i) { return i * 256u + 128u; }
 
-__device__ __forceinline__ void fixtab_store(char* lds, uint32_t G) {  // threads 0..20, after the staging
+// End table, beside it (columns 40..47 of rows 0..20): entry j for lim = j - 4 bytes of the lane's 16 before
+// the end of the CRC'd data (j = 0..20, lim clamped to -4..16): the data mask (bytes 0 .. lim - 1) and the
+// keep mask (word w all ones when it lies wholly past the frame's end, lim <= 4 w - 4: it does not step).
+__device__ __forceinline__ uint32_t endtab_addr(uint32_t j) { return j * 256u + 160u; }
+
+__device__ __forceinline__ void fixtab_store(char* lds, uint32_t G) {  // threads 0..41, after the staging
   const uint32_t t = threadIdx.x;
   if (t < (uint32_t)kFixEntries) {
     const uint4 m = front_fix(make_uint4(~0u, ~0u, ~0u, ~0u), (int)t, G), g = front_fix(make_uint4(0u, 0u, 0u, 0u), (int)t, G);
     *(uint4*)(lds + fixtab_addr(t)) = make_uint4(m.x & ~g.x, m.y & ~g.y, m.z & ~g.z, m.w & ~g.w);
     *(uint4*)(lds + fixtab_addr(t) + 16) = g;
+  } else if (t < 2u * (uint32_t)kFixEntries) {
+    const uint32_t j = t - (uint32_t)kFixEntries;
+    const int lim = (int)j - 4;
+    *(uint4*)(lds + endtab_addr(j)) = make_uint4(data_mask(lim), data_mask(lim - 4), data_mask(lim - 8), data_mask(lim - 12));
+    *(uint4*)(lds + endtab_addr(j) + 16) = make_uint4(lim <= -4 ? ~0u : 0u, lim <= 0 ? ~0u : 0u, lim <= 4 ? ~0u : 0u,
+                                                      lim <= 8 ? ~0u : 0u);
   }
 }
 
 __device__ __forceinline__ uint4 fix_piece(const char* lds, uint4 x, int p) {
+  asm("" : "+v"(p));  // (p opaque: its clamp stays one v_med3, not folded into the terms of p)
   const uint32_t i = (uint32_t)min(max(p, 0), kFixEntries - 1);
   const uint4 m = *(const uint4*)(lds + fixtab_addr(i)), g = *(const uint4*)(lds + fixtab_addr(i) + 16);
   return make_uint4(__builtin_amdgcn_bitop3_b32(x.x, m.x, g.x, 0xEA), __builtin_amdgcn_bitop3_b32(x.y, m.y, g.y, 0xEA),
@@ -204,6 +219,22 @@ __device__ __forceinline__ void chain4_masked(const Lane8& L, Chains& c, uint4 x
   c.v1 = lim > 0 ? n1 : c.v1;
   c.v2 = lim > 4 ? n2 : c.v2;
   c.v3 = lim > 8 ? n3 : c.v3;
+}
+
+// The same from the end table (lim4 = lim + 4): the data mask and the words that keep their chains in one
+// table entry, one bitop3 per word instead of a compare and a select.
+__device__ __forceinline__ void chain4_end(const Lane8& L, Chains& c, uint4 x, int lim4) {
+  asm("" : "+v"(lim4));  // (one v_med3 for the clamp)
+  const uint32_t j = (uint32_t)min(max(lim4, 0), 20);
+  const uint4 dm = *(const uint4*)(L.lds + endtab_addr(j)), kp = *(const uint4*)(L.lds + endtab_addr(j) + 16);
+  const uint32_t n0 = chain_step(L.lds, c.v0, L.K, x.x & dm.x);
+  const uint32_t n1 = chain_step(L.lds, c.v1, L.K, x.y & dm.y);
+  const uint32_t n2 = chain_step(L.lds, c.v2, L.K, x.z & dm.z);
+  const uint32_t n3 = chain_step(L.lds, c.v3, L.K, x.w & dm.w);
+  c.v0 = __builtin_amdgcn_bitop3_b32(n0, c.v0, kp.x, 0xD8);  // kp ? old : new
+  c.v1 = __builtin_amdgcn_bitop3_b32(n1, c.v1, kp.y, 0xD8);
+  c.v2 = __builtin_amdgcn_bitop3_b32(n2, c.v2, kp.z, 0xD8);
+  c.v3 = __builtin_amdgcn_bitop3_b32(n3, c.v3, kp.w, 0xD8);
 }
 
 // One 256-byte block j of a frame (pieces x0 at 16 col, x1 at 128 + 16 col, window-aligned):
@@ -446,7 +477,8 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // Geometry of set q from its words: per-lane geometry, the lane's line-0 offset, the set facts, the
   // run base (the buffer offset of the loads' resource, minus a bias: the run's first frame's start,
   // or the buffer itself for flat pairs).
-  auto geometry = [&](uint32_t q, const Rec& r, uint32_t& voff0, Set8Meta& m, uint64_t& sb, uint32_t& p14) -> uint32_t {
+  auto geometry = [&](uint32_t q, const Rec& r, uint32_t& voff0, Set8Meta& m, uint64_t& sb, uint32_t& vidx,
+                      uint32_t& voffn) -> uint32_t {
     sb = r.sb;
     const uint32_t gu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.geo);
     const uint32_t hu = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.wrel);
@@ -459,10 +491,14 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     // (the window start's low 7 bits: bytes + sb + start is 128-byte aligned)
     const uint32_t low7 = (0u - (uint32_t)(uintptr_t)p.bytes - (uint32_t)sb) & 127u;
     voff0 = live ? (((r.wrel & 0xFFFFFFu) << 7) | low7) + 16u * L.col : kV8Oob;
-    // the record index of slot 0 (+ k for slot k): P - 14, or -14 for a set with no loads (every record
-    // "negative"); opaque, so that the select stays here once per set and is not pushed into the slots
-    p14 = (live ? w_P(r.geo) : 0u) - 14u;
-    asm("" : "+v"(p14));
+    // the record index of every slot k >= 1: 16 - P (3 .. 15), or 16 for a set with no loads (past every
+    // slot's record count, kV8SlotRecords); opaque, so that the select stays here once per set and is not
+    // pushed into the slots.  The index contributes (16 - P) 128 to the address, so the slots' common offset
+    // carries 2 P 128 (voffn; the constant part is in the descriptor's base, kV8SlotBase).
+    const uint32_t P = live ? w_P(r.geo) : 0u;
+    vidx = 16u - P;
+    asm("" : "+v"(vidx));
+    voffn = voff0 + (P << 8);
     return r.geo;
   };
   // The set's loads (struct Buf13): line 0 (slot 0) and the last line (slot 12), the lines the frame
@@ -476,26 +512,32 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // while the position's last XORs still read the slot, the load goes into other registers, and each
   // straight copy of the positions ends with a different register assignment, moved back at the
   // loop's merge behind a vmcnt(1) wait)
-  auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, uint32_t p14, Buf13& b, const Chains* dep) {
+  auto load_slot = [&](int k, uint32_t voff0, uint32_t geo, uint64_t sb, uint32_t& vidx, uint32_t voffn, Buf13& b,
+                       const Chains* dep) {
     const uint32_t front = w_r(geo) + 4u;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 0, (int)0x7FFFFFF0, 0x00020000);
     if (k == 0) {
+      // (the slots' base, kV8SlotBase below the run's, with kV8SlotBase in the instruction's offset: one base
+      // for every slot's descriptor)
+      const __amdgpu_buffer_rsrc_t rs =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb - kV8SlotBase), 0, (int)0x7FFFFFF0, 0x00020000);
       const uint32_t vo = (16u * L.col + 16u <= front) ? kV8Oob : voff0;
-      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)vo, 0, kV8AuxShared);
+      const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vo + (uint32_t)kV8SlotBase), 0, kV8AuxShared);
       b.x[0] = make_uint4(v.x, v.y, v.z, v.w);
       return;
     }
-    // slot k = line k - 13 + P, as record k - 14 + P of 128-byte records from the window's line 1 (a
-    // structured load: one add per slot; a line before line 1 is a "negative" record, out of range:
-    // zeros, no request; p14 from geometry()).
+    // slot k = line k - 13 + P: a structured load of record vidx = 16 - P (stride 128) from a descriptor
+    // whose record count is 3 + k, so that the slot is in range exactly when P > 13 - k (line >= 1): lines
+    // before line 1 load zeros and make no request, and the slots share one index register (no add per
+    // slot).  Address = base + (16 - P) 128 + voff0 + 2 P 128 - 29 128 + 128 k = base + voff0 + 128 (k - 13 + P)
+    // with the -29 128 in the base (kV8SlotBase) and 128 k in the instruction's offset.
+    // (the record count set here, in the slot's own position: otherwise the 12 descriptors are hoisted out of
+    // the loop as invariants, 48 scalar registers, and spill)
+    int nrec;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(nrec) : "n"(kV8SlotRecords + k));
     const __amdgpu_buffer_rsrc_t rss =
-        __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb), 128, (int)0x7FFFFFF0, 0x00020000);
-    uint32_t idx = p14 + (uint32_t)k;
-    if (dep)
-      asm("" : "+v"(idx) : "v"(dep->v0), "v"(dep->v1), "v"(dep->v2), "v"(dep->v3));
-    else
-      asm("" : "+v"(idx));
-    const u32x4 v = ufc_struct_buffer_load_b128(rss, (int)idx, (int)(voff0 + 128u), 0,
+        __builtin_amdgcn_make_buffer_rsrc((void*)(p.bytes + sb - kV8SlotBase), 128, nrec, 0x00020000);
+    if (dep) asm("" : "+v"(vidx) : "v"(dep->v0), "v"(dep->v1), "v"(dep->v2), "v"(dep->v3));
+    const u32x4 v = ufc_struct_buffer_load_b128(rss, (int)vidx, (int)(voffn + 128u * (uint32_t)k), 0,
                                                 k == kV8Pieces - 1 ? kV8AuxShared : kV8AuxInterior);
     b.x[k] = make_uint4(v.x, v.y, v.z, v.w);
   };
@@ -593,9 +635,9 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
       const uint4 x = xin(s);
       trailer_words(s, x);
       if (s == 12)
-        chain4_masked(L, c, x, lim12);
-      else if (s == 11 && !m.penult_data)
-        chain4_masked(L, c, x, lim11);
+        chain4_end(L, c, x, lim12 + 4);
+      else if (s == 11 && !m.penult_data)  // (every word of line P - 2 lies before the frame's end: data mask only)
+        chain4(L, c, end_masked(L.lds, x, lim11));
       else
         chain4(L, c, x);
       issue(s, &c);
@@ -728,10 +770,10 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   {  // prologue: the first set's geometry and loads, the second set's record
     QG = next_q();
     const Rec r0 = load_rec(QG);
-    uint32_t P14;
-    GE = geometry(QG, r0, VO, M, SB, P14);
+    uint32_t X0, VX0;
+    GE = geometry(QG, r0, VO, M, SB, X0, VX0);
 #pragma unroll
-    for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, P14, B, nullptr);
+    for (int k = 0; k < kV8Pieces; k++) load_slot(k, VO, GE, SB, X0, VX0, B, nullptr);
     QO = next_q();
     O = load_rec(QO);
   }
@@ -755,15 +797,15 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   // (a wave's sets are valid up to its first kNoSet)
   while (QG != kNoSet) {
     // the next set: geometry from its record; the record after it
-    uint32_t VN, PN;
+    uint32_t VN, XN, VXN;
     uint64_t SBN;
     Set8Meta MN;
     const uint32_t QN = QO;
-    const uint32_t GN = geometry(QN, O, VN, MN, SBN, PN);
+    const uint32_t GN = geometry(QN, O, VN, MN, SBN, XN, VXN);
     QO = next_q();
     O = load_rec(QO);
     __builtin_amdgcn_sched_barrier(0);
-    auto issue = [&](int k, const Chains* dep = nullptr) { load_slot(k, VN, GN, SBN, PN, B, dep); };
+    auto issue = [&](int k, const Chains* dep = nullptr) { load_slot(k, VN, GN, SBN, XN, VXN, B, dep); };
     if (!M.slow) {
       compute(QG, GE, M, B, VO, SB, issue);
     } else {
