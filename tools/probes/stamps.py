@@ -1,6 +1,6 @@
 """Diagnostic (round 6, not product code): where a config-3 set's cycles go in the variable-length gate.
 
-Runs a stamp build of the library (var/stamp.so: tools/build_variant.py with s_memtime stamps at the loop
+Runs a stamp build of the library (var/stamp.so, from tools/probes/stamp_variant.py: tools/build_variant.py with s_memtime stamps at the loop
 top, after the next record's fetch, before the finish and at the end of each set; lane 0 stores the low 32
 bits of the four clocks per set into a debug array read back by ufc_dbg_read) on config 3's batch and
 prints the per-set cycle split: top (geometry, next set's record, run sort once per run), positions (the
