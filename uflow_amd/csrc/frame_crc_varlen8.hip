@@ -29,9 +29,10 @@
 //   * Sets come from runs of 64 frames sorted by line count in the wave that takes them (four one-bit
 //     radix split passes); the per-set facts come once per run from half-row reductions and ballots.
 //   * Results of a run (8 sets x 8 frames) collect in one register pair per lane and leave with
-//     hidden stores once per run.  Sets with a frame the fast path cannot take (shorter than 4 B,
-//     longer than 13 lines, at the batch edges, past its end) run byte-wise, in the same loop (the
-//     byte path keeps the 256-byte block layout of frame_crc_dev.hpp: block8 below).
+//     hidden stores once per run.  Sets with a frame the fast path cannot take (shorter than 5 B, at
+//     the batch edges, past its end) run byte-wise, in the same loop (the byte path keeps the 256-byte
+//     block layout of frame_crc_dev.hpp: block8 below); frames longer than 13 lines go from there to a
+//     second launch (frame_crc_long8_kernel, below).
 //   * Built with uniform branches left unstructured (_build.py): the set-level branches otherwise get
 //     register-copy blocks at every merge.
 #include <type_traits>
