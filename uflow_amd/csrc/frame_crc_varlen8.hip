@@ -457,13 +457,18 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
     }
     raw_load(run_nxt, raw_a, raw_b);
   };
+  // The next run is claimed and its offsets requested one set before the switch (at position 7, before
+  // that iteration issues its slots): the sort at the switch then waits for loads issued one set earlier,
+  // older than that set's 13 slot loads, a count the compiler can keep.  (Requested a whole run ahead,
+  // they sat behind ~100 younger loads, which the compiler could not count across the loop: it drained
+  // every load in flight, vmcnt(0), once per run.)
   auto next_q = [&]() -> uint32_t {
     if (pos == 8u) {
       pos = 0;
       run = run_nxt;
       sort_run(run, raw_a, raw_b, SR);
-      claim_next();
     }
+    if (pos == 7u) claim_next();
     const uint32_t q = run == kNoSet ? kNoSet : run * 8u + pos;
     pos++;
     return q;
@@ -793,7 +798,7 @@ __global__ __launch_bounds__(kV8Waves * 64) void frame_crc_varlen8_kernel(const 
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-  claim_next();  // the second run (the counter is set now)
+  // (the second run is claimed at the first run's position 7, in next_q: the counter is set now)
 
   // (a wave's sets are valid up to its first kNoSet)
   while (QG != kNoSet) {
