@@ -84,7 +84,9 @@ int ufc_ctx_create(ufc_ctx** out, int device);
 int ufc_ctx_destroy(ufc_ctx* ctx);
 /* Device scratch is kept per (context, stream) and grows only (batch parse: 14 B per frame + 2 B per
  * header slot, min(64 n, items_cap) slots; fixed seal without d_crc_out: 4 B per frame; asynchronous
- * host slots: the batch's slot bytes + 13 B per datagram).  A caller that retires a stream releases its scratch
+ * host slots: the batch's slot bytes + 13 B per datagram; variable-length gates and seals: the list of
+ * frames over 13 lines (1532 B) handed to their second launch, 4 B per frame of the largest launch
+ * (< 2^29 frames) + 256 B, and 4 B per CU of counts).  A caller that retires a stream releases its scratch
  * here, BEFORE destroying the stream: waits for the work queued on it, then frees its buffers. */
 int ufc_ctx_release_stream(ufc_ctx* ctx, void* stream);
 const char* ufc_error_string(int code);
