@@ -943,7 +943,6 @@ __global__ __launch_bounds__(kL8Waves * 64) void frame_crc_long8_kernel(const Ke
 #pragma unroll
       for (int u = 0; u < 4; u++) X[u] = load_line((uint32_t)u);
       const uint32_t pre_end = P4 - Pmin + 2u;  // steps up to a frame's line 1 (zeros, front fix, G's tail)
-      __builtin_amdgcn_s_setprio(2);  // (as the first launch: the line steps ahead of the finishes)
       for (uint32_t k0 = 0; k0 < P4; k0 += 4u) {
         const bool last = k0 + 4u == P4;  // (uniform)
 #pragma unroll
@@ -978,7 +977,6 @@ __global__ __launch_bounds__(kL8Waves * 64) void frame_crc_long8_kernel(const Ke
           }
         }
       }
-      __builtin_amdgcn_s_setprio(0);
       const uint32_t e = ((zo + 3u) >> 2) & 31u, t = (0u - zo) & 3u;
       const uint32_t crc = ~unshift8(L, group_lin8_rot(L, ch, e), t);
       if (L.col == 0u && !dead) {
